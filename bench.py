@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py -- NMPC RTI steps/s for the openKITE kite controller on MI355X.
+
+Workload (BASELINE.json configs[2]): batch = 4096 independent kite NMPC
+instances per GPU, N = 20 shooting intervals (tf = 1 s), M = 2 RK4 substeps,
+full fp64 RTI (shift -> RK4 + forward sensitivities -> Gauss-Newton
+condensing with fp64 MFMA -> interior-point QP -> expansion) per step.
+Synthetic, seeded instances; closed loop: the next step's
+measured state is the predicted state at t0 + dt of the current solution.
+
+One process per GPU (torch.distributed / RCCL); the batch shards with no
+data-path collective (weak scaling); after each step the per-instance
+results (u0 + mpc_diagnostic) are all-gathered over RCCL, as a controller
+fleet would publish them.
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_TFLOPS = 78.6        # MI355X fp64 vector = fp64 matrix (AMD spec)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--horizon", type=int, default=20)
+    ap.add_argument("--substeps", type=int, default=2)
+    ap.add_argument("--qp-iters", type=int, default=16)
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def synthetic_x0(B, offset, ctx):
+    """Seeded per-instance perturbations of launch/simulator.launch:3; theta from
+    findClosestPointOnPath on the GPU (kiteNMPF.cpp:358-391), thetadot = 0."""
+    base = np.array([4.4, 0.44, 1.73, 0.81, -1.73, -1.53, -0.46, -2.68, 0.64, -0.0289, 0.1587, 0.4304, 0.8881])
+    x = np.zeros((B, 15))
+    for b in range(B):
+        rng = np.random.default_rng(20261015 + offset + b)
+        s = base.copy()
+        s[0:3] += rng.uniform(-0.5, 0.5, 3)
+        s[3:6] += rng.uniform(-0.3, 0.3, 3)
+        s[6:9] += rng.uniform(-0.05, 0.05, 3)
+        axis = rng.normal(size=3); axis /= np.linalg.norm(axis)
+        ang = math.radians(5.0) * rng.uniform(0, 1)
+        dq = np.array([math.cos(ang / 2), *(math.sin(ang / 2) * axis)])
+        q = s[9:13]
+        qn = np.array([q[0] * dq[0] - q[1:] @ dq[1:], *(np.cross(q[1:], dq[1:]) + q[0] * dq[1:] + dq[0] * q[1:])])
+        s[9:13] = qn / np.linalg.norm(qn)
+        x[b, :13] = s
+    x[:, 13] = ctx.closest_point(x[:, 6:9])
+    return x
+
+
+def cpu_baseline(args, x0_host, budget_s):
+    """The CPU oracle (oracle/kite_oracle.cpp, OpenMP over instances) on a
+    bounded sample of the same workload: same instances, cold start + warm
+    closed-loop steps, same N/M/K.  Returns the dict for the JSON line."""
+    from oracle import ffi
+    kp = ffi.load_params()
+    cfgv = ffi.cfg_vector(ffi.node_config(N=args.horizon))
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except Exception:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, 16))
+    S = min(x0_host.shape[0], 64 * threads)
+    x = x0_host[:S].copy()
+    N = args.horizon
+    X = np.zeros((S, N + 1, 15)); U = np.zeros((S, N, 4))
+    ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=0, nthreads=threads)
+    x = X[:, 1, :].copy()
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=1, nthreads=threads)
+        x = X[:, 1, :].copy()
+        steps += 1
+        el = time.perf_counter() - t0
+        if (el >= budget_s and steps >= 2) or steps >= 200:
+            break
+    return dict(value=S * steps / el, unit="RTI steps/s", cores=threads, kind="port",
+                sample=f"{S} instances x {steps} warm closed-loop RTI steps (N={N}, M={args.substeps}, "
+                       f"K<={args.qp_iters}), oracle/kite_oracle.cpp -O3 OpenMP {threads} threads, {el:.1f} s")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import openkite_amd as ok
+    from openkite_amd import flops
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B, N = args.batch, args.horizon
+    cfg = ok.default_config(N=N, M=args.substeps, qp_iters=args.qp_iters, device=local)
+    ctx = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+
+    x0_host = synthetic_x0(B, rank * B, ctx)
+    d_x0 = torch.from_numpy(x0_host).to(dev)
+    d_u0 = torch.zeros((B, 4), dtype=torch.float64, device=dev)
+    d_traj = torch.zeros((B, N + 1, 15), dtype=torch.float64, device=dev)
+    d_diag = torch.zeros((B, 6), dtype=torch.float64, device=dev)
+    d_status = torch.zeros((B,), dtype=torch.int32, device=dev)
+    d_pub = torch.zeros((B, 10), dtype=torch.float64, device=dev)
+    gather = torch.zeros((world * B, 10), dtype=torch.float64, device=dev) if world > 1 else None
+
+    def one_step():
+        ctx.step_device(d_x0.data_ptr(), d_u0.data_ptr(), d_traj.data_ptr(), 0, d_diag.data_ptr(),
+                        d_status.data_ptr())
+        if gather is not None and not args.no_allgather:
+            d_pub[:, :4].copy_(d_u0)
+            d_pub[:, 4:].copy_(d_diag)
+            dist.all_gather_into_tensor(gather, d_pub)
+        d_x0.copy_(d_traj[:, 1, :])        # closed loop: predicted state at t0 + dt
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.timing_start(args.steps)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    nrec, ksum = ctx.timing_read()
+    kkt, iters = ctx.qp_stats()
+    status = d_status.cpu().numpy()
+
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(el_t.item())
+    total_rti = world * B * args.steps
+    value = total_rti / elapsed_max
+
+    if rank == 0:
+        mean_it = float(np.mean(iters))
+        fl = flops.rti(N, args.substeps, mean_it)
+        kernels = ["prologue", "rk4_sens", "condense", "qp"]
+        avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels}
+        dom = max(kernels, key=lambda k: avg_ms[k])
+        dom_flops = fl.get(dom, 0.0) * B
+        achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
+        rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
+        roofline = dict(bound="mfma", achieved=round(achieved, 4), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
+                        frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=None, kernel=dom,
+                        note="fp64 compute roof (vector = matrix peak on gfx950); algorithmic flops "
+                             "per launch from openkite_amd/flops.py; traffic: see profiles/")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, x0_host, args.cpu_seconds)
+        out = {
+            "metric": "NMPC RTI steps/sec, batch=4096 N=20 horizon, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "RTI steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded perturbations of launch/simulator.launch:3, umx_radian params)",
+            "config": {"workload": f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64 (BASELINE configs[2])",
+                       "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
+                       "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
+                       "allgather": bool(world > 1 and not args.no_allgather)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items()},
+            "rti_tflops_all_kernels": round(rti_flops, 4),
+            "qp_mean_iterations": round(mean_it, 3),
+            "qp_converged_frac": round(float(np.mean(kkt < 1e-8)), 5),
+            "status_nan": int(np.sum(status & 1)),
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,209 @@
+/*
+ * kite_nmpc.h -- C ABI of the MI355X-native batched kite NMPC (RTI) library.
+ *
+ * This is the drop-in boundary for openKITE's NMPC hot path.  Each entry
+ * point names the reference interface it replaces (paths relative to the
+ * openKITE repository).  The reference exchanges casadi::DM objects; here
+ * every matrix is a plain row-major double array, batched over independent
+ * NMPC instances ("batch" B).  No torch / HIP types appear in the signatures
+ * except an opaque stream handle (void*).
+ *
+ * Conventions
+ *   - Return 0 (KITE_OK) on success, a negative KITE_E* code otherwise.
+ *     Per-instance solver trouble never fails a call: it is reported in the
+ *     int32 status word of that instance (KITE_ST_* bits).
+ *   - "host" entry points take host pointers and copy in/out (synchronous).
+ *     "_device" entry points take device pointers and are asynchronous on the
+ *     context stream (kite_nmpc_set_stream).
+ *   - One context per host thread; a context is not re-entrant.  Contexts on
+ *     different devices are independent (that is how the batch shards over
+ *     GPUs: one process and one context per GPU).
+ *   - There is no CPU fallback: kite_nmpc_create fails with KITE_ENODEV when
+ *     no gfx950 device is usable.
+ *
+ * Time ordering: arrays run FORWARD in time (node 0 = t0).  The reference's
+ * Chebyshev nodes run backwards (node N = t0, chebyshev.hpp:119-127,
+ * kiteNMPF.cpp:232-235); the C++ facade KiteNMPF.hpp restores that column
+ * order for getOptimalControl()/getOptimalTrajetory().
+ */
+#ifndef KITE_NMPC_H
+#define KITE_NMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KITE_NMPC_API_VERSION 1
+
+/* ---- error codes ------------------------------------------------------ */
+#define KITE_OK        0
+#define KITE_EINVAL   (-1)   /* bad argument                                  */
+#define KITE_EHIP     (-2)   /* HIP runtime error                             */
+#define KITE_ENOMEM   (-3)   /* device or host allocation failed              */
+#define KITE_ENODEV   (-4)   /* no usable gfx950 device                       */
+#define KITE_EIO      (-5)   /* parameter file cannot be read                 */
+#define KITE_EPARSE   (-6)   /* parameter file lacks a key / bad number       */
+#define KITE_ESTATE   (-7)   /* call not valid in this context state          */
+
+/* ---- per-instance status bits (status_out) ---------------------------- */
+#define KITE_ST_NAN            1   /* non-finite value in the new iterate     */
+#define KITE_ST_QP_NOT_CONV    2   /* QP residual > 1e-8 after the cap K       */
+#define KITE_ST_MIN_SPEED      4   /* vx clamped to min_speed (nmpf_node.cpp:241-243) */
+#define KITE_ST_STATE_BOUND    8   /* predicted state outside lbx/ubx (states not
+                                      enforced in the QP: everything but vx) */
+#define KITE_ST_THETA_WRAP    16   /* theta wrapped by 2*pi (kiteNMPF.cpp:212-221) */
+
+/* ---- model parameters: kite_utils::LoadProperties (kite.cpp:7-76) ------
+ * Field order == KiteProperties (kite.h:9-93) flattened.  52 doubles.     */
+typedef struct kite_params {
+    /* geometry */
+    double b, c, AR, S, lam, St, lt, Sf, lf, Xac;
+    /* inertia */
+    double mass, Ixx, Iyy, Izz, Ixz;
+    /* aerodynamics */
+    double CL0, CL0_tail, CLa_total, CLa_wing, CLa_tail, e_oswald;
+    double CD0_total, CD0_wing, CD0_tail, CYb, CYb_vtail, Cm0, Cma;
+    double Cn0, Cnb, Cl0, Clb, CLq, Cmq, CYr, Cnr, Clr, CYp, Clp, Cnp;
+    double CLde, CYdr, Cmde, Cndr, Cldr, CDde;
+    /* tether */
+    double Lt, Ks, Kd, rx, ry, rz;
+} kite_params;
+
+/* ---- controller configuration ------------------------------------------
+ * Replaces the KiteNMPF ctor + setters + createNLP (kiteNMPF.h:14-37,
+ * kiteNMPF.cpp:18-197) and the values the ROS node feeds them
+ * (nmpf_node.cpp:30-69).  Units are physical; Sx/Su are the diagonals of the
+ * reference scaling matrices (setStateScaling / setControlScaling).      */
+typedef struct kite_nmpc_config {
+    int32_t N;            /* shooting intervals (20; 40 for long horizons)     */
+    int32_t M;            /* RK4 substeps per interval (2)                     */
+    int32_t qp_iters;     /* interior-point iteration cap K (16)               */
+    int32_t shift;        /* 1: shift the warm start by one interval per step  */
+    int32_t device;       /* HIP device ordinal                                 */
+    int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
+    int32_t reserved[2];
+    double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
+    double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */
+    double R[4];          /* control weights (kiteNMPF.cpp:33)                 */
+    double W;             /* path-speed weight (kiteNMPF.cpp:34)               */
+    double Sx[15], Su[4]; /* scaling diagonals (nmpf_node.cpp:50-51)           */
+    double lbx[15], ubx[15];  /* state bounds (nmpf_node.cpp:59-63); +-INFINITY = none */
+    double lbu[4], ubu[4];    /* control bounds (nmpf_node.cpp:45-47)          */
+    double vref;          /* physical path speed (setReferenceVelocity, nmpf_node.cpp:68) */
+    double path_radius;   /* P(theta) = rot(q)[R cos, R sin, alt] (nmpf_node.cpp:30-40) */
+    double path_altitude;
+    double path_q[4];     /* (w,x,y,z); P = vec(q^-1 (x) p (x) q)               */
+    double theta_flex;    /* +- relaxation of theta, thetadot at t0 (kiteNMPF.cpp:226) */
+    double min_speed;     /* caller-side vx clamp (nmpf_node.cpp:241-243); <= -INF disables */
+} kite_nmpc_config;
+
+/* ---- diagnostics: msg/mpc_diagnostic.msg (filled at nmpf_node.cpp:191-204) */
+typedef struct kite_mpc_diagnostic {
+    double pos_error;     /* ||Sr (P(theta0) - r0)||  (kiteNMPF.cpp:319-330)    */
+    double vel_error;     /* |Sx14 (vref - thetadot0)| (kiteNMPF.cpp:333-344)   */
+    double cost;          /* objective of the new iterate (reference sends 0)  */
+    double virt_state;    /* theta at t0 (kiteNMPF.cpp:347-355)                 */
+    double virt_ctrl;     /* Uv at t0 (unset in the reference)                  */
+    double comp_time_ms;  /* host-measured step time of the whole batch         */
+} kite_mpc_diagnostic;
+
+typedef struct kite_nmpc_ctx kite_nmpc_ctx;
+
+/* kite_utils::LoadProperties (kite.cpp:7-76).  Unlike the reference, a
+ * missing tether.rx/ry/rz defaults to 0 (the shipped umx_radian.yaml lacks
+ * them); any other missing key is KITE_EPARSE.              */
+int kite_params_load_yaml(const char* path, kite_params* out);
+
+/* Node defaults: nmpf_node.cpp:30-69 + kiteNMPF.cpp:32-34 + RTI settings.  */
+void kite_nmpc_default_config(kite_nmpc_config* cfg);
+
+/* KiteNMPF ctor + setters + createNLP (kiteNMPF.cpp:18-197).  Allocates all
+ * device buffers for `batch` instances on cfg->device.                      */
+int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg,
+                     int32_t batch, kite_nmpc_ctx** out);
+void kite_nmpc_destroy(kite_nmpc_ctx* ctx);
+const char* kite_nmpc_strerror(int code);
+
+/* setLBX/setUBX/setLBU/setUBU (kiteNMPF.h:20-27).  NULL keeps a vector.     */
+int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* ubx15,
+                         const double* lbu4, const double* ubu4);
+/* setReferenceVelocity (kiteNMPF.h:34); physical units.                     */
+int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref);
+/* disableWarmStart (kiteNMPF.h:40): the next step cold-starts.              */
+int kite_nmpc_reset(kite_nmpc_ctx* ctx);
+/* Run on this HIP stream (hipStream_t as void*; NULL = the context's own).  */
+int kite_nmpc_set_stream(kite_nmpc_ctx* ctx, void* hip_stream);
+int kite_nmpc_synchronize(kite_nmpc_ctx* ctx);
+
+/* findClosestPointOnPath (kiteNMPF.cpp:358-391), batched over `count`
+ * positions (count x 3); guess may be NULL (= 0 as in the reference).       */
+int kite_nmpc_closest_point(kite_nmpc_ctx* ctx, int32_t count, const double* pos,
+                            const double* guess, double* theta_out);
+
+/* One RTI step for the whole batch: replaces KiteNMPF::computeControl
+ * (kiteNMPF.cpp:199-316) -- NLP_Solver(ARG) becomes shift -> rk4_sens ->
+ * condense -> QP -> expand.
+ *   x0        B x 15 augmented state [v w r q theta thetadot] (physical)
+ *   u0_out    B x 4  control to apply = last column of getOptimalControl()
+ *   traj_out  B x (N+1) x 15 optimal trajectory (forward time), nullable
+ *   ctrl_out  B x N x 4 optimal controls, nullable
+ *   diag_out  B mpc_diagnostic records, nullable
+ *   status_out B status words, nullable                                      */
+int kite_nmpc_step(kite_nmpc_ctx* ctx, const double* x0, double* u0_out,
+                   double* traj_out, double* ctrl_out, kite_mpc_diagnostic* diag_out,
+                   int32_t* status_out);
+/* Same, device pointers, asynchronous on the context stream.  diag_out is
+ * B x 6 doubles in kite_mpc_diagnostic order (comp_time_ms left 0).          */
+int kite_nmpc_step_device(kite_nmpc_ctx* ctx, const double* d_x0, double* d_u0,
+                          double* d_traj, double* d_ctrl, double* d_diag, int32_t* d_status);
+
+/* Warm-start access (getOptimalTrajetory / getOptimalControl state, and
+ * NLP_X warm start injection).  Host pointers, B x (N+1) x 15 and B x N x 4. */
+int kite_nmpc_get_solution(kite_nmpc_ctx* ctx, double* traj, double* ctrl);
+int kite_nmpc_set_solution(kite_nmpc_ctx* ctx, const double* traj, const double* ctrl);
+
+/* ---- model-level entry points (KiteDynamics, kite.cpp:320-338) ---------- */
+/* getNumericDynamics: f(x,u), count x 15 states (augmented), count x 4 ctrl. */
+int kite_nmpc_dynamics(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
+                       const double* u4, double* f15);
+/* getNumericJacobian: df/dx (13 x 13) and df/du (13 x 3) of the kite ODE.    */
+int kite_nmpc_jacobian(kite_nmpc_ctx* ctx, int32_t count, const double* x13,
+                       const double* u3, double* Jx, double* Ju);
+/* RK4 integrator (kitemath.cpp:36-51, integrator.cpp:86-98) with `steps`
+ * substeps over tf: the delay-compensation predictor of nmpf_node.cpp:218.   */
+int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
+                      const double* u4, double tf, int32_t steps, double* x15_out);
+/* The hot kernel alone: x+ and S = dx+/d[x,u] over one shooting interval
+ * (h = tf/M, M substeps).  count x 15, count x 4 -> count x 15, count x 15 x 15,
+ * count x 15 x 4.                                                           */
+int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
+                       const double* u4, double tf, int32_t M, double* xnext,
+                       double* A, double* B);
+
+/* ---- introspection (tests, profiling) ---------------------------------- */
+/* Per-kernel device time [ms] of the last step (cfg.timing = 1):
+ * [prologue, rk4_sens, condense, qp, total].  n = entries available (5).    */
+int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n);
+/* Time every kernel of the next max_steps steps with a ring of HIP events
+ * (no host synchronisation between steps); timing_read waits for the last
+ * recorded step and returns the number of steps recorded, with per-kernel
+ * SUMS [ms] in sums_ms: [prologue, rk4_sens, condense, qp, total].        */
+int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps);
+int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n);
+/* QP statistics of the last step: final residual and interior-point
+ * iterations per instance (host pointers, B each; either may be NULL).    */
+int kite_nmpc_qp_stats(kite_nmpc_ctx* ctx, double* kkt, int32_t* iters);
+/* Condensed QP of one instance from the last step (scaled variables, GPU
+ * column order: [T,dE,dR]_k (3N) | Uv_k (N) | theta0 | thetadot0).
+ * H n x n, h n, C N x n, cl/cu N (+-INF = absent), n = 4N+2.               */
+int kite_nmpc_get_qp(kite_nmpc_ctx* ctx, int32_t instance, double* H, double* h,
+                     double* C, double* cl, double* cu);
+int kite_nmpc_batch(const kite_nmpc_ctx* ctx);
+int kite_nmpc_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KITE_NMPC_H */

@@ -1,0 +1,638 @@
+// kite_nmpc.cpp -- host side of the C ABI declared in include/kite_nmpc/kite_nmpc.h.
+//
+// Owns the device buffers of one batch of NMPC instances on one GPU and
+// sequences the RTI kernels (rti_kernels.hip) on a HIP stream.  There is no
+// CPU fallback: every numerical entry point runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <cctype>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "kite_nmpc/kite_nmpc.h"
+#include "rti_kernels.hpp"
+
+using kite::ModelConst;
+using kite::RtiConst;
+
+struct kite_nmpc_ctx {
+    kite_params params;
+    kite_nmpc_config cfg;
+    int B = 0;
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    bool warm = false;
+    ModelConst mc;
+    RtiConst rc;
+    // device buffers (see rti_kernels.hip for layouts)
+    double *X = nullptr, *U = nullptr, *x0 = nullptr, *AB = nullptr, *DEF = nullptr;
+    double *Hs = nullptr, *hs = nullptr, *Cr = nullptr, *cl = nullptr, *cu = nullptr, *hmax = nullptr;
+    double *u0 = nullptr, *diag = nullptr, *kkt = nullptr;
+    int32_t* status = nullptr;
+    int32_t* iters = nullptr;
+    // scratch for the model-level entry points
+    double* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool timed_step = false;
+    // event ring for timing a whole run without host syncs (kite_nmpc_timing_start)
+    std::vector<hipEvent_t> ring;
+    int ring_cap = 0, ring_used = 0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return KITE_ENOMEM;
+    return KITE_EHIP;
+}
+#define HIP_TRY(expr)                                     \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_fail(e_);        \
+    } while (0)
+
+ModelConst make_model_const(const kite_params& p) {
+    ModelConst m;
+    const double rho = kite::kRho;
+    m.inv_mass = 1.0 / p.mass;
+    m.S = p.S; m.b = p.b; m.c = p.c;
+    m.CL0 = p.CL0; m.CLa = p.CLa_total; m.CD0 = p.CD0_total;
+    m.inv_pieAR = 1.0 / (3.14159265358979323846 * p.e_oswald * p.AR);   // casadi::pi
+    m.kLq = 0.25 * p.CLq * p.c * p.S * rho;
+    m.CYb = p.CYb; m.CYdr = p.CYdr; m.kSF = 0.25 * p.b * rho * p.S;
+    m.CYr = p.CYr; m.CYp = p.CYp;
+    m.CLde = p.CLde;
+    m.Cl0 = p.Cl0; m.Clb = p.Clb; m.Cldr = p.Cldr; m.Clr = p.Clr; m.Clp = p.Clp;
+    m.kRoll = 0.25 * rho * p.b * p.b * p.S;
+    m.Cm0 = p.Cm0; m.Cma = p.Cma; m.Cmde = p.Cmde; m.Cmq = p.Cmq;
+    m.kPitch = 0.25 * p.S * p.c * p.c * rho;
+    m.Cn0 = p.Cn0; m.Cnb = p.Cnb; m.Cndr = p.Cndr; m.Cnp = p.Cnp; m.Cnr = p.Cnr;
+    m.kYaw = 0.25 * p.S * p.b * p.b * rho;
+    m.Ixx = p.Ixx; m.Iyy = p.Iyy; m.Izz = p.Izz; m.Ixz = p.Ixz;
+    const double det = p.Ixx * p.Izz - p.Ixz * p.Ixz;
+    m.Ji00 = p.Izz / det; m.Ji02 = -p.Ixz / det; m.Ji22 = p.Ixx / det; m.Ji11 = 1.0 / p.Iyy;
+    m.Lt = p.Lt; m.Ks = p.Ks; m.Kd = p.Kd; m.rx = p.rx; m.ry = p.ry; m.rz = p.rz;
+    m.half_rho = 0.5 * rho;
+    return m;
+}
+
+RtiConst make_rti_const(const kite_nmpc_config& c) {
+    RtiConst r;
+    std::memset(&r, 0, sizeof(r));
+    r.N = c.N; r.M = c.M; r.K = c.qp_iters; r.n = 4 * c.N + 2;
+    r.shift = c.shift;
+    r.lo_fin = std::isfinite(c.lbx[0]) ? 1 : 0;
+    r.hi_fin = std::isfinite(c.ubx[0]) ? 1 : 0;
+    r.dt = c.dt; r.h = c.dt / c.M;
+    for (int i = 0; i < 3; ++i) {
+        r.sqQ_dt[i] = std::sqrt(c.dt * c.Q[i]);
+        r.sqQ_T[i] = std::sqrt(c.Q[i]);
+        r.Sr[i] = c.Sx[6 + i];
+    }
+    r.sw = std::sqrt(c.dt * c.W);
+    r.sv = c.Sx[14];
+    r.vref = c.vref;
+    for (int j = 0; j < 4; ++j) {
+        r.Rdiag[j] = c.dt * c.R[j] * c.Su[j] * c.Su[j];
+        r.Rraw[j] = c.R[j];
+        r.Su[j] = c.Su[j];
+        r.lbu[j] = c.lbu[j]; r.ubu[j] = c.ubu[j];
+    }
+    r.Sx13 = c.Sx[13]; r.Sx14 = c.Sx[14];
+    for (int i = 0; i < 15; ++i) { r.lbx[i] = c.lbx[i]; r.ubx[i] = c.ubx[i]; }
+    r.flex = c.theta_flex;
+    r.min_speed = c.min_speed;
+    r.path_R = c.path_radius; r.path_alt = c.path_altitude;
+    for (int i = 0; i < 4; ++i) r.pq[i] = c.path_q[i];
+    return r;
+}
+
+int validate_config(const kite_nmpc_config& c) {
+    if (c.N < 1 || c.N > KITE_NMAX) return KITE_EINVAL;
+    if (c.M < 1 || c.M > 64) return KITE_EINVAL;
+    if (c.qp_iters < 0 || c.qp_iters > 200) return KITE_EINVAL;
+    if (!(c.dt > 0.0) || !std::isfinite(c.dt)) return KITE_EINVAL;
+    for (int i = 0; i < 15; ++i) if (!(c.Sx[i] != 0.0) || !std::isfinite(c.Sx[i])) return KITE_EINVAL;
+    for (int i = 0; i < 4; ++i) {
+        if (!(c.Su[i] != 0.0) || !std::isfinite(c.Su[i])) return KITE_EINVAL;
+        if (!std::isfinite(c.lbu[i]) || !std::isfinite(c.ubu[i]) || !(c.lbu[i] < c.ubu[i])) return KITE_EINVAL;
+    }
+    for (int i = 0; i < 3; ++i) if (!(c.Q[i] >= 0.0)) return KITE_EINVAL;
+    for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
+    if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
+    return KITE_OK;
+}
+
+int check_device(int dev) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return KITE_ENODEV;
+    if (dev < 0 || dev >= count) return KITE_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return KITE_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return KITE_ENODEV;
+    return KITE_OK;
+}
+
+int ensure_scratch(kite_nmpc_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->scratch_bytes) return KITE_OK;
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    HIP_TRY(hipMalloc(&ctx->scratch, bytes));
+    ctx->scratch_bytes = bytes;
+    return KITE_OK;
+}
+
+void free_ctx(kite_nmpc_ctx* ctx) {
+    double** bufs[] = {&ctx->X, &ctx->U, &ctx->x0, &ctx->AB, &ctx->DEF, &ctx->Hs, &ctx->hs,
+                       &ctx->Cr, &ctx->cl, &ctx->cu, &ctx->hmax, &ctx->u0, &ctx->diag, &ctx->kkt,
+                       &ctx->scratch};
+    for (double** p : bufs) if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (ctx->status) { (void)hipFree(ctx->status); ctx->status = nullptr; }
+    if (ctx->iters) { (void)hipFree(ctx->iters); ctx->iters = nullptr; }
+    for (auto& e : ctx->ev) if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
+    ctx->ring.clear();
+    if (ctx->own_stream) { (void)hipStreamDestroy(ctx->own_stream); ctx->own_stream = nullptr; }
+}
+
+// Runs the four RTI kernels on ctx->stream.  Inputs: ctx->x0 filled.
+int run_step(kite_nmpc_ctx* ctx) {
+    hipStream_t s = ctx->stream;
+    const int B = ctx->B;
+    // events: the last-step set (cfg.timing) or the next slot of the ring
+    hipEvent_t* ev = nullptr;
+    if (ctx->ring_used < ctx->ring_cap) ev = &ctx->ring[(size_t)ctx->ring_used++ * 5];
+    else if (ctx->cfg.timing) ev = ctx->ev;
+    if (ev) HIP_TRY(hipEventRecord(ev[0], s));
+    HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, ctx->x0, ctx->X, ctx->U, ctx->status, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+    HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[2], s));
+    HIP_TRY(kite::launch_condense(ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, ctx->Hs, ctx->hs, ctx->Cr,
+                                  ctx->cl, ctx->cu, ctx->hmax, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[3], s));
+    HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
+                            ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters, s));
+    if (ev) HIP_TRY(hipEventRecord(ev[4], s));
+    ctx->timed_step = (ev == ctx->ev);
+    ctx->warm = true;
+    return KITE_OK;
+}
+
+// ---- minimal YAML reader for the two-level kite parameter file -----------
+std::string trim(const std::string& s) {
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) ++a;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) --b;
+    return s.substr(a, b - a);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kite_nmpc_api_version(void) { return KITE_NMPC_API_VERSION; }
+
+const char* kite_nmpc_strerror(int code) {
+    switch (code) {
+        case KITE_OK: return "ok";
+        case KITE_EINVAL: return "invalid argument";
+        case KITE_EHIP: return "HIP runtime error";
+        case KITE_ENOMEM: return "out of memory";
+        case KITE_ENODEV: return "no usable gfx950 device";
+        case KITE_EIO: return "cannot read parameter file";
+        case KITE_EPARSE: return "parameter file: missing key or bad number";
+        case KITE_ESTATE: return "call not valid in this state";
+        default: return "unknown error";
+    }
+}
+
+int kite_params_load_yaml(const char* path, kite_params* out) {
+    if (!path || !out) return KITE_EINVAL;
+    std::ifstream f(path);
+    if (!f) return KITE_EIO;
+    std::map<std::string, double> kv;
+    std::string line, section;
+    while (std::getline(f, line)) {
+        const size_t hash = line.find('#');
+        if (hash != std::string::npos) line = line.substr(0, hash);
+        if (trim(line).empty()) continue;
+        const bool indented = std::isspace((unsigned char)line[0]);
+        const size_t colon = line.find(':');
+        if (colon == std::string::npos) return KITE_EPARSE;
+        const std::string key = trim(line.substr(0, colon));
+        const std::string val = trim(line.substr(colon + 1));
+        if (!indented) {
+            section = val.empty() ? key : std::string();
+            continue;
+        }
+        if (section.empty()) return KITE_EPARSE;
+        char* end = nullptr;
+        const double d = std::strtod(val.c_str(), &end);
+        if (val.empty() || end == val.c_str() || *end != '\0') return KITE_EPARSE;
+        kv[section + "." + key] = d;
+    }
+    struct Field { const char* key; double* dst; bool required; };
+    kite_params p;
+    std::memset(&p, 0, sizeof(p));
+    const Field fields[] = {
+        {"geometry.b", &p.b, true}, {"geometry.c", &p.c, true}, {"geometry.AR", &p.AR, true},
+        {"geometry.S", &p.S, true}, {"geometry.lam", &p.lam, true}, {"geometry.St", &p.St, true},
+        {"geometry.lt", &p.lt, true}, {"geometry.Sf", &p.Sf, true}, {"geometry.lf", &p.lf, true},
+        {"geometry.Xac", &p.Xac, true},
+        {"inertia.mass", &p.mass, true}, {"inertia.Ixx", &p.Ixx, true}, {"inertia.Iyy", &p.Iyy, true},
+        {"inertia.Izz", &p.Izz, true}, {"inertia.Ixz", &p.Ixz, true},
+        {"aerodynamic.CL0", &p.CL0, true}, {"aerodynamic.CL0_tail", &p.CL0_tail, true},
+        {"aerodynamic.CLa_total", &p.CLa_total, true}, {"aerodynamic.CLa_wing", &p.CLa_wing, true},
+        {"aerodynamic.CLa_tail", &p.CLa_tail, true}, {"aerodynamic.e_oswald", &p.e_oswald, true},
+        {"aerodynamic.CD0_total", &p.CD0_total, true}, {"aerodynamic.CD0_wing", &p.CD0_wing, true},
+        {"aerodynamic.CD0_tail", &p.CD0_tail, true}, {"aerodynamic.CYb", &p.CYb, true},
+        {"aerodynamic.CYb_vtail", &p.CYb_vtail, true}, {"aerodynamic.Cm0", &p.Cm0, true},
+        {"aerodynamic.Cma", &p.Cma, true}, {"aerodynamic.Cn0", &p.Cn0, true}, {"aerodynamic.Cnb", &p.Cnb, true},
+        {"aerodynamic.Cl0", &p.Cl0, true}, {"aerodynamic.Clb", &p.Clb, true}, {"aerodynamic.CLq", &p.CLq, true},
+        {"aerodynamic.Cmq", &p.Cmq, true}, {"aerodynamic.CYr", &p.CYr, true}, {"aerodynamic.Cnr", &p.Cnr, true},
+        {"aerodynamic.Clr", &p.Clr, true}, {"aerodynamic.CYp", &p.CYp, true}, {"aerodynamic.Clp", &p.Clp, true},
+        {"aerodynamic.Cnp", &p.Cnp, true}, {"aerodynamic.CLde", &p.CLde, true},
+        {"aerodynamic.CYdr", &p.CYdr, true}, {"aerodynamic.Cmde", &p.Cmde, true},
+        {"aerodynamic.Cndr", &p.Cndr, true}, {"aerodynamic.Cldr", &p.Cldr, true},
+        {"aerodynamic.CDde", &p.CDde, true},
+        {"tether.length", &p.Lt, true}, {"tether.Ks", &p.Ks, true}, {"tether.Kd", &p.Kd, true},
+        {"tether.rx", &p.rx, false}, {"tether.ry", &p.ry, false}, {"tether.rz", &p.rz, false},
+    };
+    for (const Field& fd : fields) {
+        auto it = kv.find(fd.key);
+        if (it == kv.end()) {
+            if (fd.required) return KITE_EPARSE;
+            *fd.dst = 0.0;
+        } else {
+            *fd.dst = it->second;
+        }
+    }
+    *out = p;
+    return KITE_OK;
+}
+
+void kite_nmpc_default_config(kite_nmpc_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    const double inf = INFINITY, pi = M_PI;
+    c->N = 20; c->M = 2; c->qp_iters = 16; c->shift = 1; c->device = 0; c->timing = 0;
+    c->dt = 0.05;
+    const double Q[3] = {1e3, 1e3, 1e4};
+    const double R[4] = {1e-4, 1e-1, 1e-1, 1e-3};
+    std::memcpy(c->Q, Q, sizeof(Q));
+    std::memcpy(c->R, R, sizeof(R));
+    c->W = 1e-3;
+    const double Sx[15] = {0.1, 1 / 3.0, 1 / 3.0, 1 / 2.0, 1 / 5.0, 1 / 2.0, 1 / 3.0, 1 / 3.0, 1 / 3.0,
+                           1.0, 1.0, 1.0, 1.0, 1 / 6.28, 1 / 6.28};
+    const double Su[4] = {1 / 0.15, 1 / 0.2618, 1 / 0.2618, 1 / 5.0};
+    std::memcpy(c->Sx, Sx, sizeof(Sx));
+    std::memcpy(c->Su, Su, sizeof(Su));
+    const double lbx[15] = {2.0, -inf, -inf, -4 * pi, -4 * pi, -4 * pi, -inf, -inf, -inf,
+                            -1.01, -1.01, -1.01, -1.01, -inf, -inf};
+    const double ubx[15] = {inf, inf, inf, 4 * pi, 4 * pi, 4 * pi, inf, inf, inf,
+                            1.01, 1.01, 1.01, 1.01, inf, inf};
+    std::memcpy(c->lbx, lbx, sizeof(lbx));
+    std::memcpy(c->ubx, ubx, sizeof(ubx));
+    const double sat = 7.0 * pi / 180.0;
+    const double lbu[4] = {0.1, -sat, -sat, -5.0};
+    const double ubu[4] = {0.15, sat, sat, 5.0};
+    std::memcpy(c->lbu, lbu, sizeof(lbu));
+    std::memcpy(c->ubu, ubu, sizeof(ubu));
+    c->vref = 4.0;
+    c->path_radius = 2.65;
+    c->path_altitude = 0.0;
+    c->path_q[0] = std::cos(pi / 8); c->path_q[1] = 0.0; c->path_q[2] = std::sin(pi / 8); c->path_q[3] = 0.0;
+    c->theta_flex = 0.78;
+    c->min_speed = 2.1;
+}
+
+int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int32_t batch,
+                     kite_nmpc_ctx** out) {
+    if (!params || !cfg || !out || batch < 1) return KITE_EINVAL;
+    *out = nullptr;
+    int rc = validate_config(*cfg);
+    if (rc) return rc;
+    rc = check_device(cfg->device);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(cfg->device));
+    kite_nmpc_ctx* ctx = new kite_nmpc_ctx();
+    ctx->params = *params;
+    ctx->cfg = *cfg;
+    ctx->B = batch;
+    ctx->device = cfg->device;
+    ctx->mc = make_model_const(*params);
+    ctx->rc = make_rti_const(*cfg);
+    const size_t B = (size_t)batch, N = (size_t)cfg->N, n = 4 * N + 2;
+    struct Alloc { double** p; size_t count; };
+    const Alloc allocs[] = {
+        {&ctx->X, B * (N + 1) * 15}, {&ctx->U, B * N * 4}, {&ctx->x0, B * 15},
+        {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13}, {&ctx->Hs, B * n * n},
+        {&ctx->hs, B * n}, {&ctx->Cr, B * N * n}, {&ctx->cl, B * N}, {&ctx->cu, B * N},
+        {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
+    };
+    for (const Alloc& a : allocs) {
+        if (hipMalloc(a.p, a.count * sizeof(double)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
+        (void)hipMemset(*a.p, 0, a.count * sizeof(double));
+    }
+    if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&ctx->iters, B * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
+    (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
+    (void)hipMemset(ctx->iters, 0, B * sizeof(int32_t));
+    if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        free_ctx(ctx); delete ctx; return KITE_EHIP;
+    }
+    ctx->stream = ctx->own_stream;
+    for (auto& e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
+    if (hipDeviceSynchronize() != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
+    *out = ctx;
+    return KITE_OK;
+}
+
+void kite_nmpc_destroy(kite_nmpc_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    free_ctx(ctx);
+    delete ctx;
+}
+
+int kite_nmpc_batch(const kite_nmpc_ctx* ctx) { return ctx ? ctx->B : KITE_EINVAL; }
+
+int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* ubx15, const double* lbu4,
+                         const double* ubu4) {
+    if (!ctx) return KITE_EINVAL;
+    kite_nmpc_config c = ctx->cfg;
+    if (lbx15) std::memcpy(c.lbx, lbx15, sizeof(c.lbx));
+    if (ubx15) std::memcpy(c.ubx, ubx15, sizeof(c.ubx));
+    if (lbu4) std::memcpy(c.lbu, lbu4, sizeof(c.lbu));
+    if (ubu4) std::memcpy(c.ubu, ubu4, sizeof(c.ubu));
+    const int rc = validate_config(c);
+    if (rc) return rc;
+    ctx->cfg = c;
+    ctx->rc = make_rti_const(c);
+    return KITE_OK;
+}
+
+int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref) {
+    if (!ctx || !std::isfinite(vref)) return KITE_EINVAL;
+    ctx->cfg.vref = vref;
+    ctx->rc = make_rti_const(ctx->cfg);
+    return KITE_OK;
+}
+
+int kite_nmpc_reset(kite_nmpc_ctx* ctx) {
+    if (!ctx) return KITE_EINVAL;
+    ctx->warm = false;
+    return KITE_OK;
+}
+
+int kite_nmpc_set_stream(kite_nmpc_ctx* ctx, void* hip_stream) {
+    if (!ctx) return KITE_EINVAL;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return KITE_OK;
+}
+
+int kite_nmpc_synchronize(kite_nmpc_ctx* ctx) {
+    if (!ctx) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return KITE_OK;
+}
+
+int kite_nmpc_step_device(kite_nmpc_ctx* ctx, const double* d_x0, double* d_u0, double* d_traj, double* d_ctrl,
+                          double* d_diag, int32_t* d_status) {
+    if (!ctx || !d_x0) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t B = ctx->B, N = ctx->cfg.N;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->x0, d_x0, B * 15 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    int rc = run_step(ctx);
+    if (rc) return rc;
+    if (d_u0) HIP_TRY(hipMemcpyAsync(d_u0, ctx->u0, B * 4 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (d_traj) HIP_TRY(hipMemcpyAsync(d_traj, ctx->X, B * (N + 1) * 15 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (d_ctrl) HIP_TRY(hipMemcpyAsync(d_ctrl, ctx->U, B * N * 4 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (d_diag) HIP_TRY(hipMemcpyAsync(d_diag, ctx->diag, B * 6 * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (d_status) HIP_TRY(hipMemcpyAsync(d_status, ctx->status, B * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return KITE_OK;
+}
+
+int kite_nmpc_step(kite_nmpc_ctx* ctx, const double* x0, double* u0_out, double* traj_out, double* ctrl_out,
+                   kite_mpc_diagnostic* diag_out, int32_t* status_out) {
+    if (!ctx || !x0) return KITE_EINVAL;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t B = ctx->B, N = ctx->cfg.N;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->x0, x0, B * 15 * sizeof(double), hipMemcpyHostToDevice, s));
+    int rc = run_step(ctx);
+    if (rc) return rc;
+    if (u0_out) HIP_TRY(hipMemcpyAsync(u0_out, ctx->u0, B * 4 * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (traj_out) HIP_TRY(hipMemcpyAsync(traj_out, ctx->X, B * (N + 1) * 15 * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (ctrl_out) HIP_TRY(hipMemcpyAsync(ctrl_out, ctx->U, B * N * 4 * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (diag_out) {
+        static_assert(sizeof(kite_mpc_diagnostic) == 6 * sizeof(double), "diagnostic layout");
+        HIP_TRY(hipMemcpyAsync(diag_out, ctx->diag, B * 6 * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    if (status_out) HIP_TRY(hipMemcpyAsync(status_out, ctx->status, B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (diag_out) {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        for (size_t b = 0; b < B; ++b) diag_out[b].comp_time_ms = ms;
+    }
+    return KITE_OK;
+}
+
+int kite_nmpc_get_solution(kite_nmpc_ctx* ctx, double* traj, double* ctrl) {
+    if (!ctx) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t B = ctx->B, N = ctx->cfg.N;
+    if (traj) HIP_TRY(hipMemcpyAsync(traj, ctx->X, B * (N + 1) * 15 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (ctrl) HIP_TRY(hipMemcpyAsync(ctrl, ctx->U, B * N * 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return KITE_OK;
+}
+
+int kite_nmpc_set_solution(kite_nmpc_ctx* ctx, const double* traj, const double* ctrl) {
+    if (!ctx || !traj || !ctrl) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t B = ctx->B, N = ctx->cfg.N;
+    HIP_TRY(hipMemcpyAsync(ctx->X, traj, B * (N + 1) * 15 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->U, ctrl, B * N * 4 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->warm = true;
+    return KITE_OK;
+}
+
+// ---- model-level entry points: host in/out, scratch on device -------------
+extern "C++" {
+namespace {
+template <class Launch>
+int run_items(kite_nmpc_ctx* ctx, const std::vector<std::pair<const double*, size_t>>& in,
+              const std::vector<std::pair<double*, size_t>>& out, Launch launch) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    size_t total = 0;
+    for (auto& p : in) total += p.second;
+    for (auto& p : out) total += p.second;
+    int rc = ensure_scratch(ctx, total * sizeof(double));
+    if (rc) return rc;
+    std::vector<double*> din, dout;
+    double* cur = ctx->scratch;
+    hipStream_t s = ctx->stream;
+    for (auto& p : in) {
+        din.push_back(cur);
+        if (p.first) HIP_TRY(hipMemcpyAsync(cur, p.first, p.second * sizeof(double), hipMemcpyHostToDevice, s));
+        cur += p.second;
+    }
+    for (auto& p : out) { dout.push_back(cur); cur += p.second; }
+    HIP_TRY(launch(din, dout, s));
+    for (size_t i = 0; i < out.size(); ++i)
+        if (out[i].first)
+            HIP_TRY(hipMemcpyAsync(out[i].first, dout[i], out[i].second * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KITE_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int kite_nmpc_dynamics(kite_nmpc_ctx* ctx, int32_t count, const double* x15, const double* u4, double* f15) {
+    if (!ctx || count < 1 || !x15 || !u4 || !f15) return KITE_EINVAL;
+    const size_t c = count;
+    return run_items(ctx, {{x15, c * 15}, {u4, c * 4}}, {{f15, c * 15}},
+                     [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
+                         return kite::launch_dynamics(ctx->mc, count, i[0], i[1], o[0], s);
+                     });
+}
+
+int kite_nmpc_jacobian(kite_nmpc_ctx* ctx, int32_t count, const double* x13, const double* u3, double* Jx,
+                       double* Ju) {
+    if (!ctx || count < 1 || !x13 || !u3 || !Jx || !Ju) return KITE_EINVAL;
+    const size_t c = count;
+    return run_items(ctx, {{x13, c * 13}, {u3, c * 3}}, {{Jx, c * 169}, {Ju, c * 39}},
+                     [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
+                         return kite::launch_jacobian(ctx->mc, count, i[0], i[1], o[0], o[1], s);
+                     });
+}
+
+int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15, const double* u4, double tf,
+                      int32_t steps, double* x15_out) {
+    if (!ctx || count < 1 || !x15 || !u4 || !x15_out || steps < 1 || !std::isfinite(tf)) return KITE_EINVAL;
+    const size_t c = count;
+    const double h = tf / steps;
+    return run_items(ctx, {{x15, c * 15}, {u4, c * 4}}, {{x15_out, c * 15}},
+                     [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
+                         return kite::launch_predict(ctx->mc, count, i[0], i[1], h, steps, o[0], s);
+                     });
+}
+
+int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15, const double* u4, double tf,
+                       int32_t M, double* xnext, double* A, double* Bm) {
+    if (!ctx || count < 1 || !x15 || !u4 || !xnext || !A || !Bm || M < 1 || !std::isfinite(tf)) return KITE_EINVAL;
+    const size_t c = count;
+    const double h = tf / M;
+    return run_items(ctx, {{x15, c * 15}, {u4, c * 4}}, {{xnext, c * 15}, {A, c * 225}, {Bm, c * 60}},
+                     [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
+                         return kite::launch_rk4_sens_items(ctx->mc, count, M, h, i[0], i[1], o[0], o[1], o[2], s);
+                     });
+}
+
+int kite_nmpc_closest_point(kite_nmpc_ctx* ctx, int32_t count, const double* pos, const double* guess,
+                            double* theta_out) {
+    if (!ctx || count < 1 || !pos || !theta_out) return KITE_EINVAL;
+    const size_t c = count;
+    std::vector<double> g;
+    if (!guess) g.assign(c, 0.0);
+    return run_items(ctx, {{pos, c * 3}, {guess ? guess : g.data(), c}}, {{theta_out, c}},
+                     [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
+                         return kite::launch_closest_point(ctx->rc, count, i[0], i[1], o[0], s);
+                     });
+}
+
+int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n) {
+    if (!ctx || !ms || n < 1) return KITE_EINVAL;
+    if (!ctx->timed_step) return KITE_ESTATE;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipEventSynchronize(ctx->ev[4]));
+    float v[5];
+    for (int i = 0; i < 4; ++i) HIP_TRY(hipEventElapsedTime(&v[i], ctx->ev[i], ctx->ev[i + 1]));
+    HIP_TRY(hipEventElapsedTime(&v[4], ctx->ev[0], ctx->ev[4]));
+    const int m = n < 5 ? n : 5;
+    for (int i = 0; i < m; ++i) ms[i] = v[i];
+    return m;
+}
+
+int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
+    if (!ctx || max_steps < 0) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t need = (size_t)max_steps * 5;
+    while (ctx->ring.size() < need) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        ctx->ring.push_back(e);
+    }
+    ctx->ring_cap = max_steps;
+    ctx->ring_used = 0;
+    return KITE_OK;
+}
+
+int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n) {
+    if (!ctx || !sums_ms || n < 1) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    double acc[5] = {0, 0, 0, 0, 0};
+    const int used = ctx->ring_used;
+    if (used > 0) HIP_TRY(hipEventSynchronize(ctx->ring[(size_t)used * 5 - 1]));
+    for (int i = 0; i < used; ++i) {
+        hipEvent_t* ev = &ctx->ring[(size_t)i * 5];
+        float v;
+        for (int k = 0; k < 4; ++k) {
+            HIP_TRY(hipEventElapsedTime(&v, ev[k], ev[k + 1]));
+            acc[k] += v;
+        }
+        HIP_TRY(hipEventElapsedTime(&v, ev[0], ev[4]));
+        acc[4] += v;
+    }
+    const int m = n < 5 ? n : 5;
+    for (int i = 0; i < m; ++i) sums_ms[i] = acc[i];
+    ctx->ring_cap = 0;
+    ctx->ring_used = 0;
+    return used;
+}
+
+int kite_nmpc_qp_stats(kite_nmpc_ctx* ctx, double* kkt, int32_t* iters) {
+    if (!ctx) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t B = ctx->B;
+    if (kkt) HIP_TRY(hipMemcpyAsync(kkt, ctx->kkt, B * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (iters) HIP_TRY(hipMemcpyAsync(iters, ctx->iters, B * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return KITE_OK;
+}
+
+int kite_nmpc_get_qp(kite_nmpc_ctx* ctx, int32_t instance, double* H, double* h, double* C, double* cl,
+                     double* cu) {
+    if (!ctx || instance < 0 || instance >= ctx->B) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t N = ctx->cfg.N, n = 4 * N + 2, b = instance;
+    hipStream_t s = ctx->stream;
+    if (H) HIP_TRY(hipMemcpyAsync(H, ctx->Hs + b * n * n, n * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (h) HIP_TRY(hipMemcpyAsync(h, ctx->hs + b * n, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (C) HIP_TRY(hipMemcpyAsync(C, ctx->Cr + b * N * n, N * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (cl) HIP_TRY(hipMemcpyAsync(cl, ctx->cl + b * N, N * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (cu) HIP_TRY(hipMemcpyAsync(cu, ctx->cu + b * N, N * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KITE_OK;
+}
+
+}  // extern "C"

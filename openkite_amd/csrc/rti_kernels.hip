@@ -1,0 +1,1081 @@
+// rti_kernels.hip -- batched RTI step for the openKITE kite NMPC on gfx950.
+//
+// One RTI step = k_prologue -> k_rk4_sens -> k_condense -> k_qp (see
+// DESIGN.md).  Replaces KiteNMPF::computeControl's NLP_Solver(ARG) call
+// (src/kite_control/kiteNMPF.cpp:199-316).
+//
+// Memory layout (HBM, fp64): every per-instance object is contiguous and the
+// instances are stacked (instance-major), i.e. exactly the host API layout:
+//   X   [B][N+1][15]   linearisation / solution trajectory (physical units)
+//   U   [B][N][4]
+//   AB  [B][N][13][16] d x+_kite / d [x_kite(13) | u_kite(3)]  per interval
+//   DEF [B][N][13]     multiple-shooting defects  x+(x_k,u_k) - x_{k+1}
+//   Hs  [B][n][n], hs [B][n], Cr [B][N][n], cl/cu [B][N]  condensed QP
+// with n = 4N+2 decision variables in GPU column order
+//   [T,dE,dR]_k (3N) | Uv_k (N) | theta_0 | thetadot_0.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kite_model.hpp"
+#include "rti_kernels.hpp"
+
+namespace kite {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_readlane(lo, lane);
+    hi = __builtin_amdgcn_readlane(hi, lane);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_or(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Path P(theta) = q_r^-1 (x) [0, R cos, R sin, alt] (x) q_r and dP/dtheta
+// (nmpf_node.cpp:30-40).
+__device__ __forceinline__ void path_eval(const RtiConst& C, double th, double P[3], double dP[3]) {
+    double s, c;
+    sincos(th, &s, &c);
+    const double qw = C.pq[0];
+    const V3<double> qu{C.pq[1], C.pq[2], C.pq[3]};
+    const double ww_uu = qw * qw - dot3(qu, qu);
+    V3<double> p = rot_body(qw, qu, ww_uu, V3<double>{C.path_R * c, C.path_R * s, C.path_alt});
+    V3<double> dp = rot_body(qw, qu, ww_uu, V3<double>{-C.path_R * s, C.path_R * c, 0.0});
+    P[0] = p.x; P[1] = p.y; P[2] = p.z;
+    dP[0] = dp.x; dP[1] = dp.y; dP[2] = dp.z;
+}
+
+// primal RK4 of the augmented 15-state model, M substeps of length h
+__device__ void rk4_primal(const ModelConst& P, const double* x0, const double* u, double h, int M,
+                           double* xo) {
+    double x[NX], xs[NX], acc[NX], k[NK];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) x[i] = x0[i];
+    for (int m = 0; m < M; ++m) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
+#pragma unroll 1
+        for (int st = 0; st < 4; ++st) {
+            kite_rhs<double>(P, xs, u, k);
+            const double kt = xs[14], kth = u[3];   // theta' = thetadot, thetadot' = Uv
+            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
+            const double wn = (st < 2) ? 0.5 * h : h;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) { acc[i] += wa * k[i]; xs[i] = x[i] + wn * k[i]; }
+            acc[13] += wa * kt; acc[14] += wa * kth;
+            xs[13] = x[13] + wn * kt; xs[14] = x[14] + wn * kth;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x[i] = acc[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xo[i] = x[i];
+}
+
+// ---------------------------------------------------------------------------
+// k_prologue: lane per instance.  theta wrap (kiteNMPF.cpp:209-221), min
+// speed clamp (nmpf_node.cpp:241-243), warm-start shift or cold start
+// (controls at the bound midpoint kiteNMPF.cpp:192-196, states by forward
+// simulation), x_0 pinned, theta/thetadot re-simulated exactly.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
+                                                 const double* __restrict__ x0in,
+                                                 double* __restrict__ X, double* __restrict__ U,
+                                                 int32_t* __restrict__ status) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int N = C.N;
+    double* Xb = X + (size_t)b * (N + 1) * NX;
+    double* Ub = U + (size_t)b * N * NU;
+    double x0[NX];
+    for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
+    int32_t st = 0;
+    const double twopi = 2.0 * M_PI;
+    if (x0[13] > twopi) { x0[13] -= twopi; st |= 16; }
+    else if (x0[13] < -twopi) { x0[13] += twopi; st |= 16; }
+    if (x0[0] < C.min_speed) { x0[0] = C.min_speed; st |= 4; }
+    if (!warm) {
+        for (int k = 0; k < N; ++k)
+            for (int j = 0; j < NU; ++j) Ub[k * NU + j] = 0.5 * (C.lbu[j] + C.ubu[j]);
+        for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
+        for (int k = 0; k < N; ++k) rk4_primal(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX]);
+    } else if (C.shift) {
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < NX; ++i) Xb[k * NX + i] = Xb[(k + 1) * NX + i];
+        for (int k = 0; k + 1 < N; ++k)
+            for (int j = 0; j < NU; ++j) Ub[k * NU + j] = Ub[(k + 1) * NU + j];
+    }
+    for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
+    double th = x0[13], thd = x0[14];
+    for (int k = 0; k < N; ++k) {
+        const double uv = Ub[k * NU + 3];
+        const double thn = th + C.dt * thd + 0.5 * C.dt * C.dt * uv;
+        const double thdn = thd + C.dt * uv;
+        Xb[(k + 1) * NX + 13] = thn;
+        Xb[(k + 1) * NX + 14] = thdn;
+        th = thn; thd = thdn;
+    }
+    status[b] = st;
+}
+
+// ---------------------------------------------------------------------------
+// k_rk4_sens: the hot kernel.  One lane per (instance, interval, direction);
+// a wavefront covers one shooting interval of 4 instances x 16 directions
+// (13 kite states + 3 kite controls; theta/thetadot/Uv are an exact double
+// integrator and are handled analytically in k_condense).  Each lane carries
+// value + tangent through M RK4 substeps (kitemath.cpp:36-51) and writes one
+// column of [A_k | B_k]; lane 0 of each instance writes the defect.
+// ---------------------------------------------------------------------------
+// Classic RK4 (M substeps) on value + one tangent.  One dual RHS needs ~166
+// VGPRs, so the RK4 state cannot stay in registers at 2 waves/SIMD: the
+// substep start state x (value+tangent) and the tangent half of the
+// accumulator live in LDS (SoA [component][lane], conflict-free, 312 B/lane;
+// 128-lane blocks -> 4 blocks = 8 waves per CU in 160 KiB).
+constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances x 16 dirs
+constexpr int RK_LDS = 3 * NK;            // x.v, x.t, acc.t
+__device__ __forceinline__ void rk4_dual(const ModelConst& P, Dual* x /*in/out [NK]*/, const Dual* u,
+                                         double h, int M, double (*sh)[RK_T], int tid) {
+    for (int m = 0; m < M; ++m) {
+        Dual xs[NK], kv[NK];
+        double accv[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) {
+            sh[i][tid] = x[i].v;
+            sh[NK + i][tid] = x[i].t;
+            sh[2 * NK + i][tid] = x[i].t;
+            xs[i] = x[i];
+            accv[i] = x[i].v;
+        }
+        // keep the compiler from forwarding the LDS stores back into registers
+        asm volatile("" ::: "memory");
+#pragma unroll 1
+        for (int st = 0; st < 4; ++st) {
+            kite_rhs<Dual>(P, xs, u, kv);
+            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
+            const double wn = (st < 2) ? 0.5 * h : h;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                accv[i] = fma(wa, kv[i].v, accv[i]);
+                sh[2 * NK + i][tid] = fma(wa, kv[i].t, sh[2 * NK + i][tid]);
+                xs[i] = Dual(fma(wn, kv[i].v, sh[i][tid]), fma(wn, kv[i].t, sh[NK + i][tid]));
+            }
+            asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < NK; ++i) x[i] = Dual(accv[i], sh[2 * NK + i][tid]);
+    }
+}
+
+__global__ __launch_bounds__(RK_T, 2) void k_rk4_sens(ModelConst P, int B, int N, int M, double h,
+                                                   const double* __restrict__ X,
+                                                   const double* __restrict__ U,
+                                                   double* __restrict__ AB,
+                                                   double* __restrict__ DEF) {
+    __shared__ double xsh[RK_LDS][RK_T];
+    const int d = threadIdx.x & 15;
+    const int b = blockIdx.x * (RK_T / 16) + (threadIdx.x >> 4);
+    const int k = blockIdx.y;
+    if (b >= B) return;
+    const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
+    const double* uk = U + ((size_t)b * N + k) * NU;
+    Dual x[NK], u[NKU];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) x[i] = mk(xk[i], d == i ? 1.0 : 0.0);
+#pragma unroll
+    for (int j = 0; j < NKU; ++j) u[j] = mk(uk[j], d == NK + j ? 1.0 : 0.0);
+    rk4_dual(P, x, u, h, M, xsh, threadIdx.x);
+    double* ab = AB + ((size_t)b * N + k) * (NK * 16);
+#pragma unroll
+    for (int i = 0; i < NK; ++i) ab[i * 16 + d] = x[i].t;
+    if (d == 0) {
+        const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
+        double* df = DEF + ((size_t)b * N + k) * NK;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_condense: one wavefront per instance.
+//   lane j < 3N  : column j of G (kite control (k=j/3, c=j%3)), 13 rows in VGPRs
+//   lane 3N      : affine column g (propagated defects)
+// Per node k the lanes write the Gauss-Newton residual rows W_k (3 path rows,
+// 1 path-speed row) into a 16-row LDS chunk; every 4 nodes the chunk is
+// folded into H_ext = W_ext^T W_ext (96 x 96, 21 lower 16x16 tiles held in
+// MFMA accumulators) with v_mfma_f64_16x16x4_f64.  Column n of W_ext is the
+// residual value, so H_ext[n][:] is the gradient.
+// ---------------------------------------------------------------------------
+constexpr int NP = 96;          // padded QP dimension (6 tiles of 16)
+constexpr int WLD = 112;        // LDS row stride of the W chunk (doubles): 2*WLD % 64 == 32
+constexpr int NTILE = 21;       // lower-triangular 16x16 tiles of 96x96
+
+typedef double double4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double col_scale(const RtiConst& C, int j) {
+    const int N = C.N;
+    if (j < 3 * N) return 1.0 / C.Su[j % 3];
+    if (j < 4 * N) return 1.0 / C.Su[3];
+    if (j == 4 * N) return 1.0 / C.Sx13;
+    return 1.0 / C.Sx14;
+}
+__device__ __forceinline__ double col_rdiag(const RtiConst& C, int j) {
+    const int N = C.N;
+    if (j < 3 * N) return C.Rdiag[j % 3];
+    if (j < 4 * N) return C.Rdiag[3];
+    return 0.0;
+}
+__device__ __forceinline__ double col_ubar(const RtiConst& C, const double* Ub, int j) {
+    const int N = C.N;
+    if (j < 3 * N) return Ub[(j / 3) * NU + (j % 3)];
+    if (j < 4 * N) return Ub[(j - 3 * N) * NU + 3];
+    return 0.0;
+}
+
+__global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double* __restrict__ X,
+                                                 const double* __restrict__ U,
+                                                 const double* __restrict__ AB,
+                                                 const double* __restrict__ DEF,
+                                                 double* __restrict__ Hs, double* __restrict__ hs,
+                                                 double* __restrict__ Cr, double* __restrict__ cl,
+                                                 double* __restrict__ cu, double* __restrict__ hmax) {
+    __shared__ double sA[NK * 16 + NK + 3];
+    __shared__ double Wc[16 * WLD];
+    const int b = blockIdx.x;
+    const int l = threadIdx.x;
+    const int N = C.N, n = C.n;
+    const double* Xb = X + (size_t)b * (N + 1) * NX;
+    const double* Ub = U + (size_t)b * N * NU;
+    const double* ABb = AB + (size_t)b * N * NK * 16;
+    const double* DEFb = DEF + (size_t)b * N * NK;
+
+    for (int i = l; i < 16 * WLD; i += 64) Wc[i] = 0.0;
+
+    const bool kite_lane = l < 3 * N;
+    const bool aff_lane = (l == 3 * N);
+    const int kb = l / 3, cc = l % 3;
+    const double Dl = kite_lane ? 1.0 / C.Su[cc] : 0.0;
+    double v[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) v[i] = 0.0;
+
+    double4v acc[NTILE];
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) acc[t] = double4v{0.0, 0.0, 0.0, 0.0};
+
+    // software prefetch of interval data (221 doubles -> <= 4 per lane)
+    double pf[4];
+    auto load_interval = [&](int k) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = l + 64 * q;
+            double val = 0.0;
+            if (e < NK * 16) val = ABb[(size_t)k * NK * 16 + e];
+            else if (e < NK * 16 + NK) val = DEFb[(size_t)k * NK + (e - NK * 16)];
+            pf[q] = val;
+        }
+    };
+    if (N > 0) load_interval(0);
+    __syncthreads();
+
+    for (int k = 0; k <= N; ++k) {
+        const bool last = (k == N);
+        const double* xk = Xb + k * NX;
+        const double th = xk[13], thd = xk[14];
+        double Pp[3], dP[3];
+        path_eval(C, th, Pp, dP);
+        // affine column (lane 3N) values broadcast
+        const double g0 = readlane_d(v[0], 3 * N);
+        const double g6 = readlane_d(v[6], 3 * N);
+        const double g7 = readlane_d(v[7], 3 * N);
+        const double g8 = readlane_d(v[8], 3 * N);
+        const double gr[3] = {g6, g7, g8};
+        double wp[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) wp[a] = (last ? C.sqQ_T[a] : C.sqQ_dt[a]) * C.Sr[a];
+        const double wv = last ? 0.0 : C.sw * C.sv;
+        const int row0 = 4 * (k & 3);
+
+        // kite columns: path rows -sq sr G[6+a], speed row 0
+        if (kite_lane) {
+            Wc[(row0 + 0) * WLD + l] = -wp[0] * v[6];
+            Wc[(row0 + 1) * WLD + l] = -wp[1] * v[7];
+            Wc[(row0 + 2) * WLD + l] = -wp[2] * v[8];
+            Wc[(row0 + 3) * WLD + l] = 0.0;
+        }
+        // analytic columns 3N .. n (Uv_m, theta0, thetadot0, affine)
+        if (l < N + 3) {
+            const int col = 3 * N + l;
+            double cth = 0.0, cthd = 0.0;
+            if (l < N) {
+                if (k > l) { cth = C.dt * C.dt * ((double)(k - l) - 0.5); cthd = C.dt; }
+            } else if (l == N) {
+                cth = 1.0;
+            } else if (l == N + 1) {
+                cth = (double)k * C.dt; cthd = 1.0;
+            }
+            if (l < N + 2) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLD + col] = wp[a] * dP[a] * cth;
+                Wc[(row0 + 3) * WLD + col] = -wv * cthd;
+            } else {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLD + col] = wp[a] * (Pp[a] - xk[6 + a] - gr[a]);
+                Wc[(row0 + 3) * WLD + col] = last ? 0.0 : C.sw * (C.sv * C.vref - C.sv * thd);
+            }
+        }
+        // vx bound rows (node k >= 1)
+        if (k >= 1) {
+            double* crow = Cr + ((size_t)b * N + (k - 1)) * n;
+            if (kite_lane) crow[l] = v[0] * Dl;
+            if (l < N + 2) crow[3 * N + l] = 0.0;
+            if (l == 0) {
+                const double base = xk[0] + g0;
+                cl[(size_t)b * N + k - 1] = C.lo_fin ? (C.lbx[0] - base) : -INFINITY;
+                cu[(size_t)b * N + k - 1] = C.hi_fin ? (C.ubx[0] - base) : INFINITY;
+            }
+        }
+        if (last) {
+            // zero the rows of nodes beyond N in this chunk
+            for (int r = row0 + 4; r < 16; ++r)
+                for (int cidx = l; cidx <= n; cidx += 64) Wc[r * WLD + cidx] = 0.0;
+        }
+        if ((k & 3) == 3 || last) {
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                double fr[6];
+#pragma unroll
+                for (int I = 0; I < 6; ++I) fr[I] = Wc[(4 * s + (l >> 4)) * WLD + 16 * I + (l & 15)];
+                int t = 0;
+#pragma unroll
+                for (int I = 0; I < 6; ++I) {
+#pragma unroll
+                    for (int J = 0; J <= I; ++J) {
+                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[I], fr[J], acc[t], 0, 0, 0);
+                        ++t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (last) break;
+
+        // propagate G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = l + 64 * q;
+            if (e < NK * 16 + NK) sA[e] = pf[q];
+        }
+        __syncthreads();
+        if (k + 1 < N) load_interval(k + 1);
+        if ((kite_lane && k >= kb) || aff_lane) {
+            double nv[NK];
+            if (kite_lane && k == kb) {
+#pragma unroll
+                for (int i = 0; i < NK; ++i) nv[i] = sA[i * 16 + NK + cc];
+            } else {
+#pragma unroll
+                for (int i = 0; i < NK; ++i) {
+                    double t = aff_lane ? sA[NK * 16 + i] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < NK; ++j) t = fma(sA[i * 16 + j], v[j], t);
+                    nv[i] = t;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NK; ++i) v[i] = nv[i];
+        }
+        __syncthreads();
+    }
+
+    // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar)
+    double* Hb = Hs + (size_t)b * n * n;
+    double lmax = 0.0;
+    int t = 0;
+#pragma unroll
+    for (int I = 0; I < 6; ++I) {
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = 16 * I + (l >> 4) + 4 * r;
+                const int gj = 16 * J + (l & 15);
+                const double a = acc[t][r];
+                if (gi < n && gj < n) {
+                    double hv = a;
+                    if (gi == gj) hv += col_rdiag(C, gi);
+                    hv *= col_scale(C, gi) * col_scale(C, gj);
+                    Hb[(size_t)gi * n + gj] = hv;
+                    Hb[(size_t)gj * n + gi] = hv;
+                    lmax = fmax(lmax, fabs(hv));
+                } else if (gi == n && gj < n) {
+                    hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
+                }
+            }
+            ++t;
+        }
+    }
+    lmax = wave_max(lmax);
+    if (l == 0) hmax[b] = lmax;
+}
+
+// ---------------------------------------------------------------------------
+// k_qp: one wavefront per instance.  Mehrotra predictor-corrector primal-dual
+// interior point on
+//     min 1/2 w'Hw + h'w   s.t.  lb <= w <= ub,  cl <= C w <= cu
+// with a relative freeze (IPM_FREEZE) and cap K, then the expansion
+// dx_{k+1} = A_k dx_k + B_k du_k + d_k, the trajectory update, diagnostics
+// (kiteNMPF.cpp:319-355) and status.
+// The normal matrix is factored in LDS (packed lower triangle).
+// ---------------------------------------------------------------------------
+constexpr int NMAX = 4 * KITE_NMAX + 2;                 // 82
+constexpr int NPACK = NMAX * (NMAX + 1) / 2;             // 3403
+constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
+
+__device__ __forceinline__ int pk(int i, int c) { return (i * (i + 1)) / 2 + c; }
+
+// row of element e in a row-wise packed lower triangle
+__device__ __forceinline__ int tri_row(int e) {
+    int r = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    if ((r + 1) * (r + 2) / 2 <= e) ++r;
+    if (r * (r + 1) / 2 > e) --r;
+    return r;
+}
+
+struct QPState {
+    // per-lane slots: variable i = l + 64*s (s = 0,1)
+    double w[2], lb[2], ub[2], h[2], sl[2], zl[2], su[2], zu[2];
+    double rd[2], rpl[2], rpu[2];
+    // general rows: lane k < N
+    double clo, chi, slo, zlo, shi, zhi, rplo, rphi, cw;
+};
+
+__global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
+                                           const double* __restrict__ Hs, const double* __restrict__ hs,
+                                           const double* __restrict__ Cr, const double* __restrict__ clp,
+                                           const double* __restrict__ cup, const double* __restrict__ hmaxp,
+                                           const double* __restrict__ AB, const double* __restrict__ DEF,
+                                           double* __restrict__ X, double* __restrict__ U,
+                                           double* __restrict__ u0_out, double* __restrict__ diag,
+                                           int32_t* __restrict__ status, double* __restrict__ kkt_out,
+                                           int32_t* __restrict__ iters_out) {
+    __shared__ double Lp[NPACK];
+    __shared__ double sC[KITE_NMAX * NMAX];
+    __shared__ double vec[NMAX + 2];
+    __shared__ double col[NMAX];
+    __shared__ double dinv[NMAX];
+
+    const int b = blockIdx.x;
+    const int l = threadIdx.x;
+    const int N = C.N, n = C.n;
+    const double* Hb = Hs + (size_t)b * n * n;
+    const double* Crb = Cr + (size_t)b * N * n;
+    double* Xb = X + (size_t)b * (N + 1) * NX;
+    double* Ub = U + (size_t)b * N * NU;
+
+    for (int e = l; e < N * n; e += 64) sC[e] = Crb[e];
+
+    QPState q;
+    const bool has_lo = C.lo_fin != 0, has_hi = C.hi_fin != 0;
+    const int nI = 2 * n + N * ((has_lo ? 1 : 0) + (has_hi ? 1 : 0));
+    const bool row_lane = l < N;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int i = l + 64 * s;
+        double lo = 0.0, hi = 0.0, hv = 0.0;
+        if (i < n) {
+            if (i < 3 * N) {
+                const int k = i / 3, c = i % 3;
+                lo = C.Su[c] * (C.lbu[c] - Ub[k * NU + c]);
+                hi = C.Su[c] * (C.ubu[c] - Ub[k * NU + c]);
+            } else if (i < 4 * N) {
+                const int k = i - 3 * N;
+                lo = C.Su[3] * (C.lbu[3] - Ub[k * NU + 3]);
+                hi = C.Su[3] * (C.ubu[3] - Ub[k * NU + 3]);
+            } else if (i == 4 * N) {
+                lo = -C.flex * C.Sx13; hi = C.flex * C.Sx13;
+            } else {
+                lo = -C.flex * C.Sx14; hi = C.flex * C.Sx14;
+            }
+            hv = hs[(size_t)b * n + i];
+        }
+        q.lb[s] = lo; q.ub[s] = hi; q.h[s] = hv;
+        const double mar = 0.1 * (hi - lo);
+        double w0 = 0.0;
+        if (w0 < lo + mar) w0 = lo + mar;
+        if (w0 > hi - mar) w0 = hi - mar;
+        q.w[s] = (i < n) ? w0 : 0.0;
+        q.sl[s] = fmax(q.w[s] - lo, IPM_S0);
+        q.su[s] = fmax(hi - q.w[s], IPM_S0);
+        q.zl[s] = IPM_Z0; q.zu[s] = IPM_Z0;
+    }
+    q.clo = row_lane ? clp[(size_t)b * N + l] : 0.0;
+    q.chi = row_lane ? cup[(size_t)b * N + l] : 0.0;
+    const double dscale = 1.0 / (1.0 + hmaxp[b]);
+
+    // --- helpers ---------------------------------------------------------
+    // y = C x for row lanes, x given in vec[]
+    auto rows_times = [&]() -> double {
+        double t = 0.0;
+        if (row_lane) {
+            const double* cr = sC + l * n;
+            for (int j = 0; j < n; ++j) t = fma(cr[j], vec[j], t);
+        }
+        return t;
+    };
+    // out_s = C^T y (y given in vec[] for rows)
+    auto rows_T = [&](double out[2]) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = l + 64 * s;
+            double t = 0.0;
+            if (i < n)
+                for (int k = 0; k < N; ++k) t = fma(sC[k * n + i], vec[k], t);
+            out[s] = t;
+        }
+    };
+    auto put_vec2 = [&](const double a[2]) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) { const int i = l + 64 * s; if (i < n) vec[i] = a[s]; }
+    };
+
+    // initial slacks of general rows
+    put_vec2(q.w);
+    __syncthreads();
+    q.cw = rows_times();
+    q.slo = row_lane && has_lo ? fmax(q.cw - q.clo, IPM_S0) : 1.0;
+    q.shi = row_lane && has_hi ? fmax(q.chi - q.cw, IPM_S0) : 1.0;
+    q.zlo = row_lane && has_lo ? IPM_Z0 : 0.0;
+    q.zhi = row_lane && has_hi ? IPM_Z0 : 0.0;
+    __syncthreads();
+
+    double resid = 0.0;
+    auto residuals = [&]() -> double {
+        // vec <- w ; Hw (column sweep, H symmetric), Cw
+        put_vec2(q.w);
+        __syncthreads();
+        double hw[2] = {0.0, 0.0};
+        for (int j = 0; j < n; ++j) {
+            const double wj = vec[j];
+            const double* hr = Hb + (size_t)j * n;
+            hw[0] = fma(hr[l < n ? l : 0], wj, hw[0]);
+            if (l + 64 < n) hw[1] = fma(hr[l + 64], wj, hw[1]);
+        }
+        q.cw = rows_times();
+        __syncthreads();
+        if (row_lane) vec[l] = (has_lo ? q.zlo : 0.0) - (has_hi ? q.zhi : 0.0);
+        __syncthreads();
+        double ctz[2];
+        rows_T(ctz);
+        __syncthreads();
+        double rmax = 0.0, mu = 0.0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = l + 64 * s;
+            if (i < n) {
+                q.rd[s] = hw[s] + q.h[s] - (q.zl[s] - q.zu[s]) - ctz[s];
+                q.rpl[s] = q.w[s] - q.lb[s] - q.sl[s];
+                q.rpu[s] = q.ub[s] - q.w[s] - q.su[s];
+                rmax = fmax(rmax, fabs(q.rd[s]) * dscale);
+                rmax = fmax(rmax, fmax(fabs(q.rpl[s]), fabs(q.rpu[s])));
+                mu += q.sl[s] * q.zl[s] + q.su[s] * q.zu[s];
+            } else {
+                q.rd[s] = 0.0; q.rpl[s] = 0.0; q.rpu[s] = 0.0;
+            }
+        }
+        q.rplo = 0.0; q.rphi = 0.0;
+        if (row_lane) {
+            if (has_lo) { q.rplo = q.cw - q.clo - q.slo; rmax = fmax(rmax, fabs(q.rplo)); mu += q.slo * q.zlo; }
+            if (has_hi) { q.rphi = q.chi - q.cw - q.shi; rmax = fmax(rmax, fabs(q.rphi)); mu += q.shi * q.zhi; }
+        }
+        rmax = wave_max(rmax);
+        mu = wave_sum(mu) / (double)nI;
+        resid = fmax(rmax, mu);
+        return mu;
+    };
+
+    // Cholesky of the packed matrix in Lp (in place, lower)
+    auto cholesky = [&]() {
+        for (int j = 0; j < n; ++j) {
+            const double piv = Lp[pk(j, j)];
+            const double dj = sqrt(piv);
+            const double inv = 1.0 / dj;
+            __syncthreads();
+            if (l == 0) { Lp[pk(j, j)] = dj; dinv[j] = inv; }
+            for (int i = j + 1 + l; i < n; i += 64) {
+                const double vv = Lp[pk(i, j)] * inv;
+                Lp[pk(i, j)] = vv;
+                col[i - j - 1] = vv;
+            }
+            __syncthreads();
+            const int m = n - j - 1;
+            const int T = m * (m + 1) / 2;
+            for (int e = l; e < T; e += 64) {
+                const int ip = tri_row(e);
+                const int cp = e - ip * (ip + 1) / 2;
+                const int idx = pk(j + 1 + ip, j + 1 + cp);
+                Lp[idx] = fma(-col[ip], col[cp], Lp[idx]);
+            }
+            __syncthreads();
+        }
+    };
+    // x <- M^-1 x with x in per-lane slots (2)
+    auto chol_solve = [&](double x[2]) {
+        for (int k = 0; k < n; ++k) {
+            double xk;
+            if (k < 64) { xk = readlane_d(x[0], k) * dinv[k]; if (l == k) x[0] = xk; }
+            else { xk = readlane_d(x[1], k - 64) * dinv[k]; if (l == k - 64) x[1] = xk; }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int i = l + 64 * s;
+                if (i > k && i < n) x[s] = fma(-Lp[pk(i, k)], xk, x[s]);
+            }
+        }
+        for (int k = n - 1; k >= 0; --k) {
+            double xk;
+            if (k < 64) { xk = readlane_d(x[0], k) * dinv[k]; if (l == k) x[0] = xk; }
+            else { xk = readlane_d(x[1], k - 64) * dinv[k]; if (l == k - 64) x[1] = xk; }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int i = l + 64 * s;
+                if (i < k) x[s] = fma(-Lp[pk(k, i)], xk, x[s]);
+            }
+        }
+    };
+
+    double sgl[2], sgu[2], sglo = 0.0, sghi = 0.0;
+    // Newton solve for complementarity rhs rc; returns directions
+    struct Dir { double dw[2], dsl[2], dsu[2], dzl[2], dzu[2], dslo, dshi, dzlo, dzhi; };
+    auto newton = [&](const double rcl[2], const double rcu[2], double rclo, double rchi, Dir& D) {
+        double t_lo = 0.0, t_hi = 0.0;
+        if (row_lane) {
+            if (has_lo) t_lo = rclo / q.slo - sglo * q.rplo;
+            if (has_hi) t_hi = rchi / q.shi - sghi * q.rphi;
+        }
+        __syncthreads();
+        if (row_lane) vec[l] = t_lo - t_hi;
+        __syncthreads();
+        double ct[2];
+        rows_T(ct);
+        double r[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = l + 64 * s;
+            if (i < n) {
+                const double tl = rcl[s] / q.sl[s] - sgl[s] * q.rpl[s];
+                const double tu = rcu[s] / q.su[s] - sgu[s] * q.rpu[s];
+                r[s] = -q.rd[s] + (tl - tu) + ct[s];
+            } else {
+                r[s] = 0.0;
+            }
+        }
+        chol_solve(r);
+        __syncthreads();
+        put_vec2(r);
+        __syncthreads();
+        const double cdw = rows_times();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            D.dw[s] = r[s];
+            D.dsl[s] = r[s] + q.rpl[s];
+            D.dsu[s] = -r[s] + q.rpu[s];
+            D.dzl[s] = (rcl[s] - q.zl[s] * D.dsl[s]) / q.sl[s];
+            D.dzu[s] = (rcu[s] - q.zu[s] * D.dsu[s]) / q.su[s];
+        }
+        D.dslo = 0.0; D.dshi = 0.0; D.dzlo = 0.0; D.dzhi = 0.0;
+        if (row_lane) {
+            if (has_lo) { D.dslo = cdw + q.rplo; D.dzlo = (rclo - q.zlo * D.dslo) / q.slo; }
+            if (has_hi) { D.dshi = -cdw + q.rphi; D.dzhi = (rchi - q.zhi * D.dshi) / q.shi; }
+        }
+    };
+    auto max_step = [&](const Dir& D) -> double {
+        double a = 1.0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = l + 64 * s;
+            if (i < n) {
+                if (D.dsl[s] < 0.0) a = fmin(a, -q.sl[s] / D.dsl[s]);
+                if (D.dsu[s] < 0.0) a = fmin(a, -q.su[s] / D.dsu[s]);
+                if (D.dzl[s] < 0.0) a = fmin(a, -q.zl[s] / D.dzl[s]);
+                if (D.dzu[s] < 0.0) a = fmin(a, -q.zu[s] / D.dzu[s]);
+            }
+        }
+        if (row_lane) {
+            if (has_lo) {
+                if (D.dslo < 0.0) a = fmin(a, -q.slo / D.dslo);
+                if (D.dzlo < 0.0) a = fmin(a, -q.zlo / D.dzlo);
+            }
+            if (has_hi) {
+                if (D.dshi < 0.0) a = fmin(a, -q.shi / D.dshi);
+                if (D.dzhi < 0.0) a = fmin(a, -q.zhi / D.dzhi);
+            }
+        }
+        return wave_min(a);
+    };
+
+    int iters = C.K;
+    for (int it = 0; it < C.K; ++it) {
+        const double mu = residuals();
+        if (resid < IPM_FREEZE) { iters = it; break; }
+        // sigma = z/s and the normal matrix H + A' Sigma A into Lp
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            sgl[s] = q.zl[s] / q.sl[s];
+            sgu[s] = q.zu[s] / q.su[s];
+        }
+        sglo = (row_lane && has_lo) ? q.zlo / q.slo : 0.0;
+        sghi = (row_lane && has_hi) ? q.zhi / q.shi : 0.0;
+        __syncthreads();
+        if (row_lane) vec[l] = sglo + sghi;
+        __syncthreads();
+        for (int rr = 0; rr < n; ++rr) {
+            const double* hr = Hb + (size_t)rr * n;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = l + 64 * s;
+                if (c <= rr) {
+                    double m = hr[c];
+                    for (int k = 0; k < N; ++k) m = fma(sC[k * n + rr] * vec[k], sC[k * n + c], m);
+                    if (c == rr) m += sgl[s] + sgu[s];
+                    Lp[pk(rr, c)] = m;
+                }
+            }
+        }
+        __syncthreads();
+        cholesky();
+        // predictor
+        double rcl[2], rcu[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) { rcl[s] = -q.sl[s] * q.zl[s]; rcu[s] = -q.su[s] * q.zu[s]; }
+        double rclo = -q.slo * q.zlo, rchi = -q.shi * q.zhi;
+        Dir Da;
+        newton(rcl, rcu, rclo, rchi, Da);
+        const double aa = max_step(Da);
+        double mua = 0.0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int i = l + 64 * s;
+            if (i < n)
+                mua += (q.sl[s] + aa * Da.dsl[s]) * (q.zl[s] + aa * Da.dzl[s]) +
+                       (q.su[s] + aa * Da.dsu[s]) * (q.zu[s] + aa * Da.dzu[s]);
+        }
+        if (row_lane) {
+            if (has_lo) mua += (q.slo + aa * Da.dslo) * (q.zlo + aa * Da.dzlo);
+            if (has_hi) mua += (q.shi + aa * Da.dshi) * (q.zhi + aa * Da.dzhi);
+        }
+        mua = wave_sum(mua) / (double)nI;
+        double sigma = mua / mu;
+        sigma = sigma * sigma * sigma;
+        // corrector
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            rcl[s] = -q.sl[s] * q.zl[s] - Da.dsl[s] * Da.dzl[s] + sigma * mu;
+            rcu[s] = -q.su[s] * q.zu[s] - Da.dsu[s] * Da.dzu[s] + sigma * mu;
+        }
+        rclo = row_lane && has_lo ? -q.slo * q.zlo - Da.dslo * Da.dzlo + sigma * mu : 0.0;
+        rchi = row_lane && has_hi ? -q.shi * q.zhi - Da.dshi * Da.dzhi + sigma * mu : 0.0;
+        Dir Dc;
+        newton(rcl, rcu, rclo, rchi, Dc);
+        const double a = fmin(1.0, IPM_TAU * max_step(Dc));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            q.w[s] += a * Dc.dw[s];
+            q.sl[s] += a * Dc.dsl[s]; q.su[s] += a * Dc.dsu[s];
+            q.zl[s] += a * Dc.dzl[s]; q.zu[s] += a * Dc.dzu[s];
+        }
+        if (row_lane) {
+            if (has_lo) { q.slo += a * Dc.dslo; q.zlo += a * Dc.dzlo; }
+            if (has_hi) { q.shi += a * Dc.dshi; q.zhi += a * Dc.dzhi; }
+        }
+    }
+    // final residual (also when frozen: residuals() already ran)
+    residuals();
+    const double kkt = resid;
+
+    // ---- expansion and trajectory update ------------------------------------
+    // physical step dw = D w_s into vec
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int i = l + 64 * s;
+        if (i < n) vec[i] = q.w[s] * col_scale(C, i);
+    }
+    __syncthreads();
+    const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
+    // theta / thetadot rows (exact double integrator), lane = node
+    for (int k = l; k <= N; k += 64) {
+        double dth = dth0 + (double)k * C.dt * dthd0, dthd = dthd0;
+        for (int m = 0; m < k; ++m) {
+            const double du = vec[3 * N + m];
+            dth += C.dt * C.dt * ((double)(k - m) - 0.5) * du;
+            dthd += C.dt * du;
+        }
+        Xb[k * NX + 13] += dth;
+        Xb[k * NX + 14] += dthd;
+    }
+    // controls
+    for (int e = l; e < N * NU; e += 64) {
+        const int k = e / NU, c = e % NU;
+        Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
+    }
+    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row)
+    {
+        double dx = 0.0;
+        const double* ABb = AB + (size_t)b * N * NK * 16;
+        const double* DEFb = DEF + (size_t)b * N * NK;
+        for (int k = 0; k < N; ++k) {
+            __syncthreads();
+            if (l < NK) col[l] = dx;
+            __syncthreads();
+            if (l < NK) {
+                const double* ar = ABb + ((size_t)k * NK + l) * 16;
+                double t = DEFb[(size_t)k * NK + l];
+                for (int j = 0; j < NK; ++j) t = fma(ar[j], col[j], t);
+                for (int c = 0; c < 3; ++c) t = fma(ar[NK + c], vec[3 * k + c], t);
+                dx = t;
+                Xb[(k + 1) * NX + l] += dx;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- diagnostics, cost, status -------------------------------------------
+    double cost = 0.0;
+    int bad = 0, bound = 0;
+    for (int k = l; k <= N; k += 64) {
+        const double* xk = Xb + k * NX;
+        double Pp[3], dP[3];
+        path_eval(C, xk[13], Pp, dP);
+        const bool last = (k == N);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double r = (last ? C.sqQ_T[a] : C.sqQ_dt[a]) * C.Sr[a] * (Pp[a] - xk[6 + a]);
+            cost += r * r;
+        }
+        if (!last) {
+            const double rv = C.sw * (C.sv * C.vref - C.sv * xk[14]);
+            cost += rv * rv;
+            for (int c = 0; c < NU; ++c) {
+                const double su = C.Su[c] * Ub[k * NU + c];
+                cost += C.dt * C.Rraw[c] * su * su;
+            }
+        }
+        for (int i = 0; i < NX; ++i) if (!isfinite(xk[i])) bad = 1;
+        if (k < N) for (int c = 0; c < NU; ++c) if (!isfinite(Ub[k * NU + c])) bad = 1;
+        if (k >= 1)
+            for (int i = 1; i < 13; ++i) if (xk[i] < C.lbx[i] || xk[i] > C.ubx[i]) bound = 1;
+    }
+    cost = wave_sum(cost);
+    bad = wave_or(bad);
+    bound = wave_or(bound);
+    if (l == 0) {
+        double Pp[3], dP[3];
+        path_eval(C, Xb[13], Pp, dP);
+        double pe = 0.0;
+        for (int a = 0; a < 3; ++a) { const double e = C.Sr[a] * (Pp[a] - Xb[6 + a]); pe += e * e; }
+        double* dg = diag + (size_t)b * 6;
+        dg[0] = sqrt(pe);
+        dg[1] = fabs(C.sv * C.vref - C.sv * Xb[14]);
+        dg[2] = cost;
+        dg[3] = Xb[13];
+        dg[4] = Ub[3];
+        dg[5] = kkt;
+        int32_t st = status[b];
+        if (bad) st |= 1;
+        if (!(kkt < 1e-8)) st |= 2;
+        if (bound && !bad) st |= 8;
+        status[b] = st;
+        if (kkt_out) kkt_out[b] = kkt;
+        if (iters_out) iters_out[b] = iters;
+        for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// model-level utility kernels (lane per item)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64, 2) void k_dynamics(ModelConst P, int count, const double* __restrict__ x,
+                           const double* __restrict__ u, double* __restrict__ f) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    double xx[NK], uu[NKU], ff[NK];
+    for (int j = 0; j < NK; ++j) xx[j] = x[(size_t)i * NX + j];
+    for (int j = 0; j < NKU; ++j) uu[j] = u[(size_t)i * NU + j];
+    kite_rhs<double>(P, xx, uu, ff);
+    for (int j = 0; j < NK; ++j) f[(size_t)i * NX + j] = ff[j];
+    f[(size_t)i * NX + 13] = x[(size_t)i * NX + 14];
+    f[(size_t)i * NX + 14] = u[(size_t)i * NU + 3];
+}
+
+// lane = (item, direction): 16 directions per item
+__global__ __launch_bounds__(256, 2) void k_jacobian(ModelConst P, int count, const double* __restrict__ x,
+                           const double* __restrict__ u, double* __restrict__ Jx,
+                           double* __restrict__ Ju) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = g >> 4, d = g & 15;
+    if (i >= count) return;
+    Dual xx[NK], uu[NKU], ff[NK];
+    for (int j = 0; j < NK; ++j) xx[j] = mk(x[(size_t)i * NK + j], d == j ? 1.0 : 0.0);
+    for (int j = 0; j < NKU; ++j) uu[j] = mk(u[(size_t)i * NKU + j], d == NK + j ? 1.0 : 0.0);
+    kite_rhs<Dual>(P, xx, uu, ff);
+    for (int r = 0; r < NK; ++r) {
+        if (d < NK) Jx[((size_t)i * NK + r) * NK + d] = ff[r].t;
+        else Ju[((size_t)i * NK + r) * NKU + (d - NK)] = ff[r].t;
+    }
+}
+
+__global__ __launch_bounds__(64, 2) void k_predict(ModelConst P, int count, const double* __restrict__ x,
+                          const double* __restrict__ u, double h, int steps,
+                          double* __restrict__ xo) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    double xx[NX], uu[NU], yy[NX];
+    for (int j = 0; j < NX; ++j) xx[j] = x[(size_t)i * NX + j];
+    for (int j = 0; j < NU; ++j) uu[j] = u[(size_t)i * NU + j];
+    rk4_primal(P, xx, uu, h, steps, yy);
+    for (int j = 0; j < NX; ++j) xo[(size_t)i * NX + j] = yy[j];
+}
+
+// rk4 with sensitivities for independent (x,u) items (API kite_nmpc_rk4_sens):
+// same lane mapping as k_rk4_sens; writes full 15x15 / 15x4 blocks with the
+// exact theta/thetadot/Uv rows and columns.
+__global__ __launch_bounds__(RK_T, 2) void k_rk4_sens_items(ModelConst P, int count, int M, double h,
+                                                           const double* __restrict__ x,
+                                                           const double* __restrict__ u,
+                                                           double* __restrict__ xo,
+                                                           double* __restrict__ A,
+                                                           double* __restrict__ Bm) {
+    __shared__ double xsh[RK_LDS][RK_T];
+    const int d = threadIdx.x & 15;
+    const int i = blockIdx.x * (RK_T / 16) + (threadIdx.x >> 4);
+    if (i >= count) return;
+    const double* xi = x + (size_t)i * NX;
+    const double* ui = u + (size_t)i * NU;
+    Dual xv[NK], uu[NKU];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) xv[j] = mk(xi[j], d == j ? 1.0 : 0.0);
+#pragma unroll
+    for (int j = 0; j < NKU; ++j) uu[j] = mk(ui[j], d == NK + j ? 1.0 : 0.0);
+    rk4_dual(P, xv, uu, h, M, xsh, threadIdx.x);
+    const double T = h * M;
+    double* Ai = A + (size_t)i * NX * NX;
+    double* Bi = Bm + (size_t)i * NX * NU;
+    for (int r = 0; r < NK; ++r) {
+        if (d < NK) Ai[r * NX + d] = xv[r].t;
+        else Bi[r * NU + (d - NK)] = xv[r].t;
+    }
+    if (d == 0) {
+        for (int r = 0; r < NK; ++r) { Ai[r * NX + 13] = 0.0; Ai[r * NX + 14] = 0.0; Bi[r * NU + 3] = 0.0; }
+        for (int c = 0; c < NX; ++c) { Ai[13 * NX + c] = 0.0; Ai[14 * NX + c] = 0.0; }
+        Ai[13 * NX + 13] = 1.0; Ai[13 * NX + 14] = T; Ai[14 * NX + 14] = 1.0;
+        for (int c = 0; c < NU; ++c) { Bi[13 * NU + c] = 0.0; Bi[14 * NU + c] = 0.0; }
+        Bi[13 * NU + 3] = 0.5 * T * T; Bi[14 * NU + 3] = T;
+        double* xoi = xo + (size_t)i * NX;
+        for (int r = 0; r < NK; ++r) xoi[r] = xv[r].v;
+        xoi[13] = xi[13] + T * xi[14] + 0.5 * T * T * ui[3];
+        xoi[14] = xi[14] + T * ui[3];
+    }
+}
+
+// findClosestPointOnPath (kiteNMPF.cpp:358-391): gradient steps on
+// 0.5*||P(theta) - pos|| with step 0.25, tol 1e-2, <= 11 updates.
+__global__ __launch_bounds__(64, 2) void k_closest_point(RtiConst C, int count, const double* __restrict__ pos,
+                                const double* __restrict__ guess, double* __restrict__ theta) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const double px = pos[(size_t)i * 3], py = pos[(size_t)i * 3 + 1], pz = pos[(size_t)i * 3 + 2];
+    auto grad = [&](double th) {
+        double P[3], dP[3];
+        path_eval(C, th, P, dP);
+        const double e0 = P[0] - px, e1 = P[1] - py, e2 = P[2] - pz;
+        const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+        return 0.5 * (e0 * dP[0] + e1 * dP[1] + e2 * dP[2]) / nrm;
+    };
+    double th = guess ? guess[i] : 0.0;
+    double g = grad(th);
+    if (fabs(g) < 1e-2) { th = M_PI_2 + 0.1; g = grad(th); }
+    int counter = 0;
+    while (fabs(g) >= 1e-2) {
+        ++counter;
+        th -= 0.25 * g;
+        g = grad(th);
+        if (counter > 10) break;
+    }
+    theta[i] = th;
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
+                           double* X, double* U, int32_t* status, hipStream_t s) {
+    hipLaunchKernelGGL(k_prologue, dim3((B + 63) / 64), dim3(64), 0, s, P, C, B, warm, x0, X, U, status);
+    return hipGetLastError();
+}
+hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
+                           double* AB, double* DEF, hipStream_t s) {
+    hipLaunchKernelGGL(k_rk4_sens, dim3((B + RK_T / 16 - 1) / (RK_T / 16), C.N), dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
+    return hipGetLastError();
+}
+hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
+                           const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
+                           double* hmax, hipStream_t s) {
+    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), 0, s, C, B, X, U, AB, DEF, Hs, hs, Cr, cl, cu, hmax);
+    return hipGetLastError();
+}
+hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
+                     const double* Cr, const double* cl, const double* cu, const double* hmax,
+                     const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
+                     int32_t* status, double* kkt, int32_t* iters, hipStream_t s) {
+    hipLaunchKernelGGL(k_qp, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U, u0,
+                       diag, status, kkt, iters);
+    return hipGetLastError();
+}
+hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_dynamics, dim3((count + 63) / 64), dim3(64), 0, s, P, count, x, u, f);
+    return hipGetLastError();
+}
+hipError_t launch_jacobian(const ModelConst& P, int count, const double* x, const double* u, double* Jx,
+                           double* Ju, hipStream_t s) {
+    hipLaunchKernelGGL(k_jacobian, dim3((count * 16 + 255) / 256), dim3(256), 0, s, P, count, x, u, Jx, Ju);
+    return hipGetLastError();
+}
+hipError_t launch_predict(const ModelConst& P, int count, const double* x, const double* u, double h,
+                          int steps, double* xo, hipStream_t s) {
+    hipLaunchKernelGGL(k_predict, dim3((count + 63) / 64), dim3(64), 0, s, P, count, x, u, h, steps, xo);
+    return hipGetLastError();
+}
+hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h, const double* x,
+                                 const double* u, double* xo, double* A, double* Bm, hipStream_t s) {
+    hipLaunchKernelGGL(k_rk4_sens_items, dim3((count + RK_T / 16 - 1) / (RK_T / 16)), dim3(RK_T), 0, s, P, count, M, h, x, u, xo, A, Bm);
+    return hipGetLastError();
+}
+hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,
+                                double* theta, hipStream_t s) {
+    hipLaunchKernelGGL(k_closest_point, dim3((count + 63) / 64), dim3(64), 0, s, C, count, pos, guess, theta);
+    return hipGetLastError();
+}
+
+}  // namespace kite

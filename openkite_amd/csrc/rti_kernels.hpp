@@ -1,0 +1,57 @@
+// rti_kernels.hpp -- internal interface between the C ABI (kite_nmpc.cpp) and
+// the gfx950 kernels (rti_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kite_model.hpp"
+
+// Largest horizon the fused condense/QP kernels are built for (LDS budget of
+// the wave-per-instance QP).  n = 4N+2 <= 82 decision variables.
+#define KITE_NMAX 20
+
+namespace kite {
+
+// Everything the RTI kernels need besides the model, precomputed on the host
+// from kite_nmpc_config (kernel argument, < 1 KiB).
+struct RtiConst {
+    int N, M, K, n;
+    int shift, lo_fin, hi_fin, pad_;
+    double dt, h;
+    double sqQ_dt[3];   // sqrt(dt Q_i)   stage path weights
+    double sqQ_T[3];    // sqrt(Q_i)      Mayer path weights (kiteNMPF.cpp:141)
+    double sw;          // sqrt(dt W)
+    double Sr[3];       // Sx[6..8]
+    double sv;          // Sx[14]
+    double vref;        // physical
+    double Rdiag[4];    // dt R_c Su_c^2
+    double Rraw[4];     // R_c
+    double Su[4], Sx13, Sx14;
+    double lbx[15], ubx[15], lbu[4], ubu[4];
+    double flex, min_speed;
+    double path_R, path_alt, pq[4];
+};
+
+hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
+                           double* X, double* U, int32_t* status, hipStream_t s);
+hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
+                           double* AB, double* DEF, hipStream_t s);
+hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
+                           const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
+                           double* hmax, hipStream_t s);
+hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
+                     const double* Cr, const double* cl, const double* cu, const double* hmax,
+                     const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
+                     int32_t* status, double* kkt, int32_t* iters, hipStream_t s);
+hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,
+                           hipStream_t s);
+hipError_t launch_jacobian(const ModelConst& P, int count, const double* x, const double* u, double* Jx,
+                           double* Ju, hipStream_t s);
+hipError_t launch_predict(const ModelConst& P, int count, const double* x, const double* u, double h,
+                          int steps, double* xo, hipStream_t s);
+hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h, const double* x,
+                                 const double* u, double* xo, double* A, double* Bm, hipStream_t s);
+hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,
+                                double* theta, hipStream_t s);
+
+}  // namespace kite

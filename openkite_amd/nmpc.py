@@ -1,0 +1,443 @@
+"""Python host side of the MI355X kite NMPC: ctypes binding of the C ABI
+(include/kite_nmpc/kite_nmpc.h) plus a ``KiteNMPF`` class that mirrors the
+reference controller API (src/kite_control/kiteNMPF.h:10-118).
+
+Every numerical call goes to libkite_nmpc.so on the GPU; if the library is
+missing or no gfx950 device is present the calls raise -- there is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkite_nmpc.so")
+REPO = os.path.dirname(_HERE)
+DEFAULT_PARAMS = os.path.join(REPO, "data", "umx_radian.yaml")
+
+KITE_OK, KITE_EINVAL, KITE_EHIP, KITE_ENOMEM, KITE_ENODEV, KITE_EIO, KITE_EPARSE, KITE_ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
+ST_NAN, ST_QP_NOT_CONV, ST_MIN_SPEED, ST_STATE_BOUND, ST_THETA_WRAP = 1, 2, 4, 8, 16
+
+_PARAM_FIELDS = ["b", "c", "AR", "S", "lam", "St", "lt", "Sf", "lf", "Xac",
+                 "mass", "Ixx", "Iyy", "Izz", "Ixz",
+                 "CL0", "CL0_tail", "CLa_total", "CLa_wing", "CLa_tail", "e_oswald",
+                 "CD0_total", "CD0_wing", "CD0_tail", "CYb", "CYb_vtail", "Cm0", "Cma",
+                 "Cn0", "Cnb", "Cl0", "Clb", "CLq", "Cmq", "CYr", "Cnr", "Clr", "CYp", "Clp", "Cnp",
+                 "CLde", "CYdr", "Cmde", "Cndr", "Cldr", "CDde",
+                 "Lt", "Ks", "Kd", "rx", "ry", "rz"]
+
+
+class KiteParams(ctypes.Structure):
+    """kite_params (KiteProperties flattened, kite.h:9-93)."""
+    _fields_ = [(f, ctypes.c_double) for f in _PARAM_FIELDS]
+
+    def as_array(self) -> np.ndarray:
+        return np.array([getattr(self, f) for f in _PARAM_FIELDS], dtype=np.float64)
+
+
+class NmpcConfig(ctypes.Structure):
+    _fields_ = [
+        ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("qp_iters", ctypes.c_int32), ("shift", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("timing", ctypes.c_int32), ("reserved", ctypes.c_int32 * 2),
+        ("dt", ctypes.c_double), ("Q", ctypes.c_double * 3), ("R", ctypes.c_double * 4), ("W", ctypes.c_double),
+        ("Sx", ctypes.c_double * 15), ("Su", ctypes.c_double * 4),
+        ("lbx", ctypes.c_double * 15), ("ubx", ctypes.c_double * 15),
+        ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4),
+        ("vref", ctypes.c_double), ("path_radius", ctypes.c_double), ("path_altitude", ctypes.c_double),
+        ("path_q", ctypes.c_double * 4), ("theta_flex", ctypes.c_double), ("min_speed", ctypes.c_double),
+    ]
+
+    def to_dict(self) -> dict:
+        d = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            d[name] = list(v) if hasattr(v, "__len__") else v
+        return d
+
+
+class MpcDiagnostic(ctypes.Structure):
+    """msg/mpc_diagnostic.msg field order."""
+    _fields_ = [("pos_error", ctypes.c_double), ("vel_error", ctypes.c_double), ("cost", ctypes.c_double),
+                ("virt_state", ctypes.c_double), ("virt_ctrl", ctypes.c_double), ("comp_time_ms", ctypes.c_double)]
+
+
+DIAG_FIELDS = [f for f, _ in MpcDiagnostic._fields_]
+
+_lib = None
+_DP = ctypes.POINTER(ctypes.c_double)
+_IP = ctypes.POINTER(ctypes.c_int32)
+
+# every symbol of include/kite_nmpc/kite_nmpc.h with its ctypes signature
+_SIGNATURES = {
+    "kite_nmpc_api_version": (ctypes.c_int, []),
+    "kite_nmpc_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "kite_params_load_yaml": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(KiteParams)]),
+    "kite_nmpc_default_config": (None, [ctypes.POINTER(NmpcConfig)]),
+    "kite_nmpc_create": (ctypes.c_int, [ctypes.POINTER(KiteParams), ctypes.POINTER(NmpcConfig), ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "kite_nmpc_destroy": (None, [ctypes.c_void_p]),
+    "kite_nmpc_batch": (ctypes.c_int, [ctypes.c_void_p]),
+    "kite_nmpc_set_bounds": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP]),
+    "kite_nmpc_set_reference_velocity": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
+    "kite_nmpc_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "kite_nmpc_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "kite_nmpc_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "kite_nmpc_closest_point": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP]),
+    "kite_nmpc_step": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, ctypes.POINTER(MpcDiagnostic), _IP]),
+    "kite_nmpc_step_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kite_nmpc_get_solution": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP]),
+    "kite_nmpc_set_solution": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP]),
+    "kite_nmpc_dynamics": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP]),
+    "kite_nmpc_jacobian": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP]),
+    "kite_nmpc_predict": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, ctypes.c_double,
+                                         ctypes.c_int32, _DP]),
+    "kite_nmpc_rk4_sens": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, ctypes.c_double,
+                                          ctypes.c_int32, _DP, _DP, _DP]),
+    "kite_nmpc_kernel_times": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
+    "kite_nmpc_get_qp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP, _DP]),
+    "kite_nmpc_timing_start": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
+    "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
+}
+
+
+class KiteNmpcError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        msg = lib().kite_nmpc_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+        self.code = code
+
+
+def lib():
+    """Load libkite_nmpc.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C openkite_amd/csrc` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(code: int, what: str):
+    if code < 0:
+        raise KiteNmpcError(code, what)
+    return code
+
+
+def _p(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"], "float64 C-contiguous array required"
+    return a.ctypes.data_as(_DP)
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def load_properties(path: str = DEFAULT_PARAMS) -> KiteParams:
+    """kite_utils::LoadProperties (kite.cpp:7-76) via the C ABI."""
+    p = KiteParams()
+    _check(lib().kite_params_load_yaml(path.encode(), ctypes.byref(p)), f"load {path}")
+    return p
+
+
+def default_config(**overrides) -> NmpcConfig:
+    """The reference node's controller setup (nmpf_node.cpp:30-69) + RTI defaults."""
+    c = NmpcConfig()
+    lib().kite_nmpc_default_config(ctypes.byref(c))
+    for k, v in overrides.items():
+        if not hasattr(c, k):
+            raise KeyError(k)
+        cur = getattr(c, k)
+        if hasattr(cur, "__len__"):
+            for i, vi in enumerate(v):
+                cur[i] = vi
+        else:
+            setattr(c, k, v)
+    return c
+
+
+class BatchNMPC:
+    """A batch of independent NMPC instances on one GPU (one C-ABI context)."""
+
+    def __init__(self, params: Optional[KiteParams] = None, config: Optional[NmpcConfig] = None,
+                 batch: int = 1):
+        self.params = params if params is not None else load_properties()
+        self.config = config if config is not None else default_config()
+        self.batch = int(batch)
+        self.N = int(self.config.N)
+        h = ctypes.c_void_p()
+        _check(lib().kite_nmpc_create(ctypes.byref(self.params), ctypes.byref(self.config), self.batch,
+                                      ctypes.byref(h)), "kite_nmpc_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().kite_nmpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # --- configuration ----------------------------------------------------
+    def set_bounds(self, lbx=None, ubx=None, lbu=None, ubu=None):
+        args = [None if a is None else _f64(a) for a in (lbx, ubx, lbu, ubu)]
+        _check(lib().kite_nmpc_set_bounds(self._h, *[_p(a) for a in args]), "set_bounds")
+
+    def set_reference_velocity(self, v: float):
+        _check(lib().kite_nmpc_set_reference_velocity(self._h, float(v)), "set_reference_velocity")
+
+    def reset(self):
+        _check(lib().kite_nmpc_reset(self._h), "reset")
+
+    def set_stream(self, stream_ptr: int):
+        _check(lib().kite_nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),
+               "set_stream")
+
+    def synchronize(self):
+        _check(lib().kite_nmpc_synchronize(self._h), "synchronize")
+
+    # --- RTI step -------------------------------------------------------------
+    def step(self, x0: np.ndarray, want_traj: bool = True):
+        B, N = self.batch, self.N
+        x0 = _f64(x0).reshape(B, 15)
+        u0 = np.zeros((B, 4))
+        traj = np.zeros((B, N + 1, 15)) if want_traj else None
+        ctrl = np.zeros((B, N, 4)) if want_traj else None
+        diag = (MpcDiagnostic * B)()
+        status = np.zeros(B, dtype=np.int32)
+        _check(lib().kite_nmpc_step(self._h, _p(x0), _p(u0), _p(traj), _p(ctrl), diag,
+                                    status.ctypes.data_as(_IP)), "kite_nmpc_step")
+        d = np.ctypeslib.as_array(ctypes.cast(diag, _DP), shape=(B, 6)).copy()
+        return dict(u0=u0, traj=traj, ctrl=ctrl, diag=d, status=status)
+
+    def step_device(self, x0_ptr: int, u0_ptr=0, traj_ptr=0, ctrl_ptr=0, diag_ptr=0, status_ptr=0):
+        v = lambda p: ctypes.c_void_p(p) if p else None
+        _check(lib().kite_nmpc_step_device(self._h, v(x0_ptr), v(u0_ptr), v(traj_ptr), v(ctrl_ptr),
+                                           v(diag_ptr), v(status_ptr)), "kite_nmpc_step_device")
+
+    def get_solution(self):
+        traj = np.zeros((self.batch, self.N + 1, 15)); ctrl = np.zeros((self.batch, self.N, 4))
+        _check(lib().kite_nmpc_get_solution(self._h, _p(traj), _p(ctrl)), "get_solution")
+        return traj, ctrl
+
+    def set_solution(self, traj, ctrl):
+        _check(lib().kite_nmpc_set_solution(self._h, _p(_f64(traj)), _p(_f64(ctrl))), "set_solution")
+
+    def kernel_times(self):
+        ms = np.zeros(5)
+        n = _check(lib().kite_nmpc_kernel_times(self._h, _p(ms), 5), "kernel_times")
+        return dict(zip(["prologue", "rk4_sens", "condense", "qp", "total"], ms[:n]))
+
+    def timing_start(self, max_steps: int):
+        _check(lib().kite_nmpc_timing_start(self._h, int(max_steps)), "timing_start")
+
+    def timing_read(self):
+        """Per-kernel SUMS [ms] over the steps recorded since timing_start."""
+        ms = np.zeros(5)
+        n = _check(lib().kite_nmpc_timing_read(self._h, _p(ms), 5), "timing_read")
+        return n, dict(zip(["prologue", "rk4_sens", "condense", "qp", "total"], ms))
+
+    def qp_stats(self):
+        kkt = np.zeros(self.batch); it = np.zeros(self.batch, dtype=np.int32)
+        _check(lib().kite_nmpc_qp_stats(self._h, _p(kkt), it.ctypes.data_as(_IP)), "qp_stats")
+        return kkt, it
+
+    def get_qp(self, instance: int):
+        n = 4 * self.N + 2
+        H = np.zeros((n, n)); h = np.zeros(n); C = np.zeros((self.N, n)); cl = np.zeros(self.N); cu = np.zeros(self.N)
+        _check(lib().kite_nmpc_get_qp(self._h, int(instance), _p(H), _p(h), _p(C), _p(cl), _p(cu)), "get_qp")
+        return dict(H=H, h=h, C=C, cl=cl, cu=cu)
+
+    # --- model-level ----------------------------------------------------------
+    def closest_point(self, pos, guess=None):
+        pos = _f64(pos).reshape(-1, 3)
+        out = np.zeros(pos.shape[0])
+        g = None if guess is None else _f64(guess).reshape(-1)
+        _check(lib().kite_nmpc_closest_point(self._h, pos.shape[0], _p(pos), _p(g), _p(out)), "closest_point")
+        return out
+
+    def dynamics(self, x15, u4):
+        x = _f64(x15).reshape(-1, 15); u = _f64(u4).reshape(-1, 4)
+        f = np.zeros_like(x)
+        _check(lib().kite_nmpc_dynamics(self._h, x.shape[0], _p(x), _p(u), _p(f)), "dynamics")
+        return f
+
+    def jacobian(self, x13, u3):
+        x = _f64(x13).reshape(-1, 13); u = _f64(u3).reshape(-1, 3)
+        Jx = np.zeros((x.shape[0], 13, 13)); Ju = np.zeros((x.shape[0], 13, 3))
+        _check(lib().kite_nmpc_jacobian(self._h, x.shape[0], _p(x), _p(u), _p(Jx), _p(Ju)), "jacobian")
+        return Jx, Ju
+
+    def predict(self, x15, u4, tf: float, steps: int = 1):
+        x = _f64(x15).reshape(-1, 15); u = _f64(u4).reshape(-1, 4)
+        xo = np.zeros_like(x)
+        _check(lib().kite_nmpc_predict(self._h, x.shape[0], _p(x), _p(u), float(tf), int(steps), _p(xo)), "predict")
+        return xo
+
+    def rk4_sens(self, x15, u4, tf: float, M: int):
+        x = _f64(x15).reshape(-1, 15); u = _f64(u4).reshape(-1, 4)
+        c = x.shape[0]
+        xo = np.zeros((c, 15)); A = np.zeros((c, 15, 15)); Bm = np.zeros((c, 15, 4))
+        _check(lib().kite_nmpc_rk4_sens(self._h, c, _p(x), _p(u), float(tf), int(M), _p(xo), _p(A), _p(Bm)),
+               "rk4_sens")
+        return xo, A, Bm
+
+
+@dataclass
+class _ReturnStatus:
+    status: int
+
+    @property
+    def return_status(self) -> str:
+        if self.status & ST_NAN:
+            return "Invalid_Number_Detected"
+        if self.status & ST_QP_NOT_CONV:
+            return "Maximum_Iterations_Exceeded"
+        return "Solve_Succeeded"
+
+
+class KiteNMPF:
+    """Mirror of the reference ``KiteNMPF`` (kiteNMPF.h:10-118) for one kite.
+
+    Setters / getters keep the reference names and semantics: matrices are
+    returned in the reference's column order, i.e. time runs backwards and the
+    LAST column of getOptimalControl() is u(t0) (nmpf_node.cpp:124).  The
+    scaling matrices are diagonal; setReferenceVelocity is physical and, as
+    in the reference, must be called after setStateScaling (it is stored in
+    physical units here so the order no longer matters).
+    """
+
+    def __init__(self, params: Optional[KiteParams] = None, N: int = 20, dt: float = 0.05, **cfg):
+        self._cfg = default_config(N=N, dt=dt, **cfg)
+        self._params = params if params is not None else load_properties()
+        self._impl: Optional[BatchNMPC] = None
+        self._traj = None
+        self._ctrl = None
+        self._diag = None
+        self._status = 0
+        self._warm = False
+
+    # setters kiteNMPF.h:20-34
+    def setLBX(self, v): self._set("lbx", v)
+    def setUBX(self, v): self._set("ubx", v)
+    def setLBU(self, v): self._set("lbu", v)
+    def setUBU(self, v): self._set("ubu", v)
+    def setLBG(self, v): pass          # collocation equality bounds: no counterpart in the RTI
+    def setUBG(self, v): pass
+
+    def setStateScaling(self, S):
+        self._set("Sx", np.diag(np.asarray(S, dtype=float)) if np.ndim(S) == 2 else S)
+
+    def setControlScaling(self, S):
+        self._set("Su", np.diag(np.asarray(S, dtype=float)) if np.ndim(S) == 2 else S)
+
+    def setReferenceVelocity(self, v):
+        self._cfg.vref = float(np.asarray(v).reshape(-1)[0])
+        if self._impl is not None:
+            self._impl.set_reference_velocity(self._cfg.vref)
+
+    def setPath(self, radius: float, altitude: float = 0.0, q=(1.0, 0.0, 0.0, 0.0)):
+        """The reference declares setPath(SX) but never defines it (kiteNMPF.h:36);
+        here the path family is the rotated circle of nmpf_node.cpp:30-40."""
+        self._cfg.path_radius = radius
+        self._cfg.path_altitude = altitude
+        for i in range(4):
+            self._cfg.path_q[i] = q[i]
+        self._impl = None
+
+    def _set(self, name, v):
+        arr = getattr(self._cfg, name)
+        for i, vi in enumerate(np.asarray(v, dtype=float).reshape(-1)):
+            arr[i] = vi
+        if self._impl is not None and name in ("lbx", "ubx", "lbu", "ubu"):
+            self._impl.set_bounds(np.array(self._cfg.lbx), np.array(self._cfg.ubx),
+                                  np.array(self._cfg.lbu), np.array(self._cfg.ubu))
+        elif self._impl is not None:
+            self._impl = None
+
+    def createNLP(self):
+        self._impl = BatchNMPC(self._params, self._cfg, 1)
+        self._warm = False
+
+    def enableWarmStart(self):
+        self._warm = True
+
+    def disableWarmStart(self):
+        self._warm = False
+        if self._impl is not None:
+            self._impl.reset()
+
+    def computeControl(self, X0):
+        """KiteNMPF::computeControl (kiteNMPF.cpp:199-316) as one RTI step."""
+        if self._impl is None:
+            self.createNLP()
+        if not self._warm:
+            self._impl.reset()
+        r = self._impl.step(np.asarray(X0, dtype=float).reshape(1, 15))
+        self._traj, self._ctrl, self._diag, self._status = r["traj"][0], r["ctrl"][0], r["diag"][0], int(r["status"][0])
+        self.enableWarmStart()
+
+    def getOptimalControl(self):
+        """4 x N, reference column order (last column = u(t0))."""
+        return None if self._ctrl is None else self._ctrl[::-1].T.copy()
+
+    def getOptimalTrajetory(self):   # [sic] kiteNMPF.h:44
+        """15 x (N+1), reference column order (last column = x(t0))."""
+        return None if self._traj is None else self._traj[::-1].T.copy()
+
+    def getPathFunction(self):
+        cfg = self._cfg
+        qw, qx, qy, qz = list(cfg.path_q)
+
+        def P(theta):
+            v = np.array([cfg.path_radius * math.cos(theta), cfg.path_radius * math.sin(theta), cfg.path_altitude])
+            u = np.array([qx, qy, qz])
+            return (qw * qw - u @ u) * v + 2 * (u @ v) * u - 2 * qw * np.cross(u, v)
+        return P
+
+    def getStats(self):
+        return {"return_status": _ReturnStatus(self._status).return_status, "status_bits": self._status}
+
+    def getPathError(self):
+        return 0.0 if self._diag is None else float(self._diag[0])
+
+    def getVelocityError(self):
+        return 0.0 if self._diag is None else float(self._diag[1])
+
+    def getVirtState(self):
+        return 0.0 if self._diag is None else float(self._diag[3])
+
+    def initialized(self):
+        return False   # never set true in the reference (kiteNMPF.cpp:46)
+
+    def findClosestPointOnPath(self, position, init_guess=0.0):
+        if self._impl is None:
+            self.createNLP()
+        return float(self._impl.closest_point(np.asarray(position, dtype=float).reshape(1, 3),
+                                              np.array([float(init_guess)]))[0])
+
+    def diagnostic(self):
+        """mpc_diagnostic record (nmpf_node.cpp:191-204)."""
+        return None if self._diag is None else dict(zip(DIAG_FIELDS, map(float, self._diag)))

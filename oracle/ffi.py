@@ -1,0 +1,273 @@
+"""ctypes front-end of the CPU oracle (oracle/kite_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.  The product (openkite_amd) never imports it.
+
+Also holds the oracle's own view of the kite parameter file and of the
+controller configuration the reference ROS node sets up
+(src/kite_control/nmpf_node.cpp:30-69, kiteNMPF.cpp:32-34).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Dict
+
+import numpy as np
+import yaml
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "liboracle.so")
+REPO = os.path.dirname(_HERE)
+DEFAULT_YAML = os.path.join(REPO, "data", "umx_radian.yaml")
+
+# parameter order == kite_oracle.cpp enum KP == include/kite_nmpc/kite_nmpc.h kite_params
+PARAM_KEYS = [
+    ("geometry", "b"), ("geometry", "c"), ("geometry", "AR"), ("geometry", "S"),
+    ("geometry", "lam"), ("geometry", "St"), ("geometry", "lt"), ("geometry", "Sf"),
+    ("geometry", "lf"), ("geometry", "Xac"),
+    ("inertia", "mass"), ("inertia", "Ixx"), ("inertia", "Iyy"), ("inertia", "Izz"), ("inertia", "Ixz"),
+    ("aerodynamic", "CL0"), ("aerodynamic", "CL0_tail"), ("aerodynamic", "CLa_total"),
+    ("aerodynamic", "CLa_wing"), ("aerodynamic", "CLa_tail"), ("aerodynamic", "e_oswald"),
+    ("aerodynamic", "CD0_total"), ("aerodynamic", "CD0_wing"), ("aerodynamic", "CD0_tail"),
+    ("aerodynamic", "CYb"), ("aerodynamic", "CYb_vtail"), ("aerodynamic", "Cm0"), ("aerodynamic", "Cma"),
+    ("aerodynamic", "Cn0"), ("aerodynamic", "Cnb"), ("aerodynamic", "Cl0"), ("aerodynamic", "Clb"),
+    ("aerodynamic", "CLq"), ("aerodynamic", "Cmq"), ("aerodynamic", "CYr"), ("aerodynamic", "Cnr"),
+    ("aerodynamic", "Clr"), ("aerodynamic", "CYp"), ("aerodynamic", "Clp"), ("aerodynamic", "Cnp"),
+    ("aerodynamic", "CLde"), ("aerodynamic", "CYdr"), ("aerodynamic", "Cmde"), ("aerodynamic", "Cndr"),
+    ("aerodynamic", "Cldr"), ("aerodynamic", "CDde"),
+    ("tether", "length"), ("tether", "Ks"), ("tether", "Kd"), ("tether", "rx"), ("tether", "ry"),
+    ("tether", "rz"),
+]
+assert len(PARAM_KEYS) == 52
+
+
+def load_params(path: str = DEFAULT_YAML) -> np.ndarray:
+    with open(path) as f:
+        doc = yaml.safe_load(f)
+    return np.array([float(doc[a][b]) for a, b in PARAM_KEYS], dtype=np.float64)
+
+
+def node_config(N: int = 20, dt: float = 0.05) -> Dict:
+    """Controller configuration of the reference ROS node (nmpf_node.cpp:30-69)."""
+    inf = math.inf
+    sat = math.radians(7.0)
+    return dict(
+        N=N, dt=dt,
+        Q=[1e3, 1e3, 1e4], R=[1e-4, 1e-1, 1e-1, 1e-3], W=1e-3,       # kiteNMPF.cpp:32-34
+        Sx=[0.1, 1 / 3.0, 1 / 3.0, 1 / 2.0, 1 / 5.0, 1 / 2.0, 1 / 3.0, 1 / 3.0, 1 / 3.0,
+            1.0, 1.0, 1.0, 1.0, 1 / 6.28, 1 / 6.28],
+        Su=[1 / 0.15, 1 / 0.2618, 1 / 0.2618, 1 / 5.0],
+        lbx=[2.0, -inf, -inf, -4 * math.pi, -4 * math.pi, -4 * math.pi, -inf, -inf, -inf,
+             -1.01, -1.01, -1.01, -1.01, -inf, -inf],
+        ubx=[inf, inf, inf, 4 * math.pi, 4 * math.pi, 4 * math.pi, inf, inf, inf,
+             1.01, 1.01, 1.01, 1.01, inf, inf],
+        lbu=[0.1, -sat, -sat, -5.0], ubu=[0.15, sat, sat, 5.0],
+        vref=4.0,
+        path_R=2.65, path_alt=0.0,
+        path_q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0],
+        flex=0.78, min_speed=2.1,
+    )
+
+
+def cfg_vector(c: Dict) -> np.ndarray:
+    v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
+         *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
+         c["flex"], c["min_speed"]]
+    a = np.array(v, dtype=np.float64)
+    assert a.size == 75
+    return a
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle not built: {LIB_PATH} (run make -C oracle)")
+        L = ctypes.CDLL(LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        i = ctypes.c_int
+        d = ctypes.c_double
+        sig = {
+            "orc_rhs": (None, [dp, dp, dp, dp]),
+            "orc_rhs_aug": (None, [dp, dp, dp, dp]),
+            "orc_rhs_jac_cs": (None, [dp, dp, dp, dp]),
+            "orc_rhs_jac_ad": (None, [dp, dp, dp, dp]),
+            "orc_rk4": (None, [dp, dp, dp, d, i, dp]),
+            "orc_rk4_sens": (None, [dp, dp, dp, d, i, dp, dp, dp]),
+            "orc_rk4_sens_cs": (None, [dp, dp, dp, d, i, dp, dp]),
+            "orc_path": (None, [dp, d, dp, dp]),
+            "orc_closest_point": (d, [dp, dp, d]),
+            "orc_build_qp": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
+            "orc_qp_solve": (d, [i, i, dp, dp, dp, dp, dp, dp, i, dp]),
+            "orc_prologue": (i, [dp, dp, i, i, dp, i, i, dp, dp, dp]),
+            "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i]),
+            "orc_traj_cost": (d, [dp, i, dp, dp]),
+            "orc_cheb_points": (None, [i, dp]),
+            "orc_cheb_D": (None, [i, dp]),
+            "orc_cheb_weights": (None, [i, dp]),
+            "orc_cheb_compD": (None, [i, i, dp]),
+            "orc_cheb_expansion": (d, [dp, i, d]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def rhs(kp, x13, u3):
+    f = np.zeros(13)
+    lib().orc_rhs(_p(kp), _p(_f64(x13)), _p(_f64(u3)), _p(f))
+    return f
+
+
+def rhs_aug(kp, x15, u4):
+    f = np.zeros(15)
+    lib().orc_rhs_aug(_p(kp), _p(_f64(x15)), _p(_f64(u4)), _p(f))
+    return f
+
+
+def rhs_jac(kp, x13, u3, method="ad"):
+    J = np.zeros((13, 16))
+    fn = lib().orc_rhs_jac_ad if method == "ad" else lib().orc_rhs_jac_cs
+    fn(_p(kp), _p(_f64(x13)), _p(_f64(u3)), _p(J))
+    return J
+
+
+def rk4(kp, x15, u4, h, M=1):
+    xo = np.zeros(15)
+    lib().orc_rk4(_p(kp), _p(_f64(x15)), _p(_f64(u4)), float(h), int(M), _p(xo))
+    return xo
+
+
+def rk4_sens(kp, x15, u4, h, M=1):
+    xo = np.zeros(15); A = np.zeros((15, 15)); B = np.zeros((15, 4))
+    lib().orc_rk4_sens(_p(kp), _p(_f64(x15)), _p(_f64(u4)), float(h), int(M), _p(xo), _p(A), _p(B))
+    return xo, A, B
+
+
+def rk4_sens_cs(kp, x15, u4, h, M=1):
+    A = np.zeros((15, 15)); B = np.zeros((15, 4))
+    lib().orc_rk4_sens_cs(_p(kp), _p(_f64(x15)), _p(_f64(u4)), float(h), int(M), _p(A), _p(B))
+    return A, B
+
+
+def path(cfgv, theta):
+    P = np.zeros(3); dP = np.zeros(3)
+    lib().orc_path(_p(cfgv), float(theta), _p(P), _p(dP))
+    return P, dP
+
+
+def closest_point(cfgv, pos, guess=0.0):
+    return lib().orc_closest_point(_p(cfgv), _p(_f64(pos)), float(guess))
+
+
+def build_qp(kp, cfgv, N, M, X, U):
+    n = 4 * N + 2
+    mmax = 2 * N
+    H = np.zeros((n, n)); h = np.zeros(n); lb = np.zeros(n); ub = np.zeros(n)
+    C = np.zeros((mmax, n)); c = np.zeros(mmax); D = np.zeros(n); g = np.zeros((N + 1, 15))
+    m = lib().orc_build_qp(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), _p(H), _p(h), _p(lb),
+                           _p(ub), _p(C), _p(c), _p(D), _p(g))
+    return dict(H=H, h=h, lb=lb, ub=ub, C=C[:m].copy(), c=c[:m].copy(), D=D, g=g, m=m)
+
+
+def qp_solve(H, h, lb, ub, C, c, K):
+    n = H.shape[0]
+    m = C.shape[0]
+    w = np.zeros(n)
+    kkt = lib().orc_qp_solve(n, m, _p(_f64(H)), _p(_f64(h)), _p(_f64(lb)), _p(_f64(ub)),
+                             _p(_f64(C.reshape(-1)) if m else np.zeros(1)),
+                             _p(_f64(c) if m else np.zeros(1)), int(K), _p(w))
+    return w, kkt
+
+
+def prologue(kp, cfgv, N, M, x0, X, U, warm, shift=1):
+    X = _f64(X).copy(); U = _f64(U).copy(); x0o = np.zeros(15)
+    st = lib().orc_prologue(_p(kp), _p(cfgv), N, M, _p(_f64(x0)), int(warm), int(shift), _p(X), _p(U), _p(x0o))
+    return st, X, U, x0o
+
+
+def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0):
+    """Batched RTI step.  x0 (B,15); X (B,N+1,15) and U (B,N,4) updated in place."""
+    B = x0.shape[0]
+    assert X.shape == (B, N + 1, 15) and U.shape == (B, N, 4)
+    assert X.dtype == np.float64 and U.dtype == np.float64 and X.flags["C_CONTIGUOUS"] and U.flags["C_CONTIGUOUS"]
+    u0 = np.zeros((B, 4)); diag = np.zeros((B, 6)); status = np.zeros(B, dtype=np.int32)
+    lib().orc_rti_step(_p(kp), _p(cfgv), N, M, K, B, int(warm), int(shift), _p(_f64(x0)), _p(X), _p(U),
+                       _p(u0), _p(diag), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                       int(nthreads))
+    return u0, diag, status
+
+
+def traj_cost(cfgv, N, X, U):
+    return lib().orc_traj_cost(_p(cfgv), N, _p(_f64(X)), _p(_f64(U)))
+
+
+def cheb_points(n):
+    x = np.zeros(n + 1); lib().orc_cheb_points(n, _p(x)); return x
+
+
+def cheb_D(n):
+    D = np.zeros((n + 1, n + 1)); lib().orc_cheb_D(n, _p(D)); return D
+
+
+def cheb_weights(n):
+    w = np.zeros(n + 1); lib().orc_cheb_weights(n, _p(w)); return w
+
+
+def cheb_compD(P, S):
+    m = S * P + 1
+    D = np.zeros((m, m)); lib().orc_cheb_compD(P, S, _p(D)); return D
+
+
+def cheb_expansion(coef, x):
+    c = _f64(coef)
+    return lib().orc_cheb_expansion(_p(c), c.size, float(x))
+
+
+# ---- synthetic benchmark inputs --------------------------
+BASE_STATE = np.array([4.4, 0.44, 1.73, 0.81, -1.73, -1.53, -0.46, -2.68, 0.64,
+                       -0.0289, 0.1587, 0.4304, 0.8881])   # launch/simulator.launch:3
+SEED0 = 20261015
+
+
+def synthetic_states(B: int, seed0: int = SEED0, offset: int = 0) -> np.ndarray:
+    """Per-instance seeded perturbations of the in-flight state (13 kite states)."""
+    out = np.zeros((B, 13))
+    for b in range(B):
+        rng = np.random.default_rng(seed0 + offset + b)
+        x = BASE_STATE.copy()
+        x[0:3] += rng.uniform(-0.5, 0.5, 3)
+        x[3:6] += rng.uniform(-0.3, 0.3, 3)
+        x[6:9] += rng.uniform(-0.05, 0.05, 3)
+        axis = rng.normal(size=3)
+        axis /= np.linalg.norm(axis)
+        ang = math.radians(5.0) * rng.uniform(0, 1)
+        dq = np.array([math.cos(ang / 2), *(math.sin(ang / 2) * axis)])
+        q = x[9:13]
+        # Hamilton product q (x) dq, then normalise
+        w1, v1 = q[0], q[1:]
+        w2, v2 = dq[0], dq[1:]
+        qn = np.array([w1 * w2 - v1 @ v2, *(np.cross(v1, v2) + w1 * v2 + w2 * v1)])
+        x[9:13] = qn / np.linalg.norm(qn)
+        out[b] = x
+    return out

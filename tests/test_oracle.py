@@ -1,0 +1,191 @@
+"""CPU tests of the parity oracle (oracle/kite_oracle.cpp).
+
+The oracle is pinned by the golden fixtures (50-digit sympy/mpmath
+restatement of kite.cpp / kitemath.cpp / chebyshev.hpp, tests/golden/) and by
+textbook Chebyshev values.  The reference's own tests hold no expected values
+(every case ends in BOOST_CHECK(true)); their inputs are reused.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import ffi
+
+RHS_TOL = 1e-13     # relative, f
+JAC_TOL = 1e-12     # relative, df/d[x,u]
+RK4_TOL = 1e-12     # relative, x+
+SENS_TOL = 1e-10    # relative, S = dx+/d[x,u]
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+def test_rhs_matches_golden(kp, golden):
+    for c in golden["rhs"]:
+        assert rel(ffi.rhs(kp, c["x"], c["u"]), c["f"]) < RHS_TOL, c["source"]
+
+
+@pytest.mark.parametrize("method", ["ad", "cs"])
+def test_jacobian_matches_golden(kp, golden, method):
+    for c in golden["rhs"]:
+        J = ffi.rhs_jac(kp, c["x"], c["u"], method)
+        assert rel(J, c["J"]) < JAC_TOL, (method, c["source"])
+
+
+def test_rk4_and_sensitivities_match_golden(kp, golden):
+    for c in golden["rk4"]:
+        xo, A, B = ffi.rk4_sens(kp, c["x"], c["u"], c["tf"] / c["M"], c["M"])
+        assert rel(xo, c["xnext"]) < RK4_TOL, c["source"]
+        assert rel(A, c["A"]) < SENS_TOL, c["source"]
+        assert rel(B, c["B"]) < SENS_TOL, c["source"]
+
+
+def test_reference_rk4_call(kp, golden):
+    """ODESolver::rk4_solve one step of 7 s (kite_model_test.cpp:58-75): diverges
+    to ~1e62, which both the oracle and the 50-digit restatement reproduce."""
+    c = golden["rk4_reference_call"]
+    xo = ffi.rk4(kp, c["x"], c["u"], c["tf"], 1)
+    np.testing.assert_allclose(xo, c["xnext"], rtol=1e-12)
+
+
+def test_ad_matches_complex_step_through_rk4(kp):
+    x = np.r_[ffi.BASE_STATE, 1.1, -0.2]
+    for M in (1, 2, 4):
+        _, A, B = ffi.rk4_sens(kp, x, [0.12, 0.05, -0.03, 1.5], 0.05 / M, M)
+        Ac, Bc = ffi.rk4_sens_cs(kp, x, [0.12, 0.05, -0.03, 1.5], 0.05 / M, M)
+        assert rel(A, Ac) < 1e-13 and rel(B, Bc) < 1e-13
+
+
+def test_theta_double_integrator_is_exact(kp):
+    """theta' = thetadot, thetadot' = Uv (kiteNMPF.cpp:62-73): RK4 is exact."""
+    x = np.r_[ffi.BASE_STATE, 0.7, -1.3]
+    u = [0.12, 0.0, 0.0, 2.5]
+    T = 0.05
+    xo, A, B = ffi.rk4_sens(kp, x, u, T / 2, 2)
+    assert xo[13] == pytest.approx(0.7 - 1.3 * T + 0.5 * T * T * 2.5, abs=1e-15)
+    assert xo[14] == pytest.approx(-1.3 + T * 2.5, abs=1e-15)
+    assert A[13, 14] == pytest.approx(T) and B[13, 3] == pytest.approx(0.5 * T * T) and B[14, 3] == pytest.approx(T)
+
+
+def test_chebyshev_golden_and_textbook(golden):
+    ch = golden["chebyshev"]
+    for n, D in ch["D"].items():
+        np.testing.assert_allclose(ffi.cheb_D(int(n)), D, atol=1e-12)
+    for n, w in ch["weights"].items():
+        np.testing.assert_allclose(ffi.cheb_weights(int(n)), w, atol=1e-14)
+        assert sum(w) == pytest.approx(2.0)
+    for n, x in ch["points"].items():
+        np.testing.assert_allclose(ffi.cheb_points(int(n)), x, atol=1e-15)
+    np.testing.assert_allclose(ffi.cheb_compD(5, 2), ch["compD"]["5x2"], atol=1e-12)
+    np.testing.assert_allclose(ffi.cheb_compD(2, 3), ch["compD"]["2x3"], atol=1e-12)
+    tb = ch["textbook"]
+    np.testing.assert_allclose(ffi.cheb_D(2), tb["D2"], atol=1e-14)
+    np.testing.assert_allclose(ffi.cheb_D(5)[0], tb["D5_row0"], atol=1e-6)
+    np.testing.assert_allclose(ffi.cheb_weights(5), tb["w5"], atol=1e-6)
+    np.testing.assert_allclose(ffi.cheb_weights(2), tb["w2"], atol=1e-14)
+    e = ch["expansion"]
+    assert ffi.cheb_expansion(e["coef"], e["x"]) == pytest.approx(e["value"])
+    assert math.isinf(ffi.lib().orc_cheb_expansion(None, 0, 0.5))
+
+
+def test_path_matches_golden(golden):
+    pc = golden["path"]
+    cfg = ffi.node_config()
+    cv = ffi.cfg_vector(cfg)
+    assert cfg["path_R"] == pc["radius"]
+    for c in pc["cases"]:
+        P, dP = ffi.path(cv, c["theta"])
+        np.testing.assert_allclose(P, c["P"], atol=1e-14)
+        np.testing.assert_allclose(dP, c["dP"], atol=1e-14)
+
+
+def test_closest_point_behaviour(cfgv):
+    """kiteNMPF.cpp:358-391: <= 11 gradient steps of 0.25 on 0.5*||P - r||."""
+    P, _ = ffi.path(cfgv, 1.0)
+    pos = P * 1.05
+    th = ffi.closest_point(cfgv, pos, 0.3)
+    d_before = np.linalg.norm(ffi.path(cfgv, 0.3)[0] - pos)
+    d_after = np.linalg.norm(ffi.path(cfgv, th)[0] - pos)
+    assert d_after < d_before and abs(th - 1.0) < 0.3
+    # a guess with (near) zero gradient triggers the restart from pi/2 + 0.1
+    P0, _ = ffi.path(cfgv, 0.0)
+    th2 = ffi.closest_point(cfgv, P0 * 1.05, 0.0)
+    assert th2 != 0.0 and abs(th2) < math.pi / 2 + 0.1
+
+
+def _cold_instances(kp, cv, B):
+    xs = ffi.synthetic_states(B)
+    x0 = np.zeros((B, 15))
+    x0[:, :13] = xs
+    for b in range(B):
+        x0[b, 13] = ffi.closest_point(cv, xs[b, 6:9])
+    return x0
+
+
+def test_prologue_cold_and_shift(kp, cfgv):
+    N, M = 20, 2
+    x0 = _cold_instances(kp, cfgv, 1)[0]
+    st, X, U, xo = ffi.prologue(kp, cfgv, N, M, x0, np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+    assert st == 0
+    np.testing.assert_array_equal(X[0], x0)
+    np.testing.assert_allclose(U, np.tile([0.125, 0.0, 0.0, 0.0], (N, 1)))
+    for k in range(N):   # cold start is a forward simulation: no defects
+        np.testing.assert_allclose(X[k + 1], ffi.rk4(kp, X[k], U[k], 0.025, 2), atol=1e-14)
+    # warm + shift: X_k <- X_{k+1}, last node duplicated, theta re-simulated
+    U2 = U.copy(); U2[:, 3] = np.linspace(-1, 1, N)
+    x1 = X[1].copy(); x1[13] = 7.0        # > 2 pi -> wrapped
+    st, Xs, Us, xo = ffi.prologue(kp, cfgv, N, M, x1, X, U2, warm=1)
+    assert st & 16
+    assert xo[13] == pytest.approx(7.0 - 2 * math.pi)
+    np.testing.assert_array_equal(Xs[5, :13], X[6, :13])
+    np.testing.assert_array_equal(Us[:-1], U2[1:])
+
+
+def test_min_speed_clamp(kp, cfgv):
+    x0 = _cold_instances(kp, cfgv, 1)[0]
+    x0[0] = 1.0
+    st, X, U, xo = ffi.prologue(kp, cfgv, 20, 2, x0, np.zeros((21, 15)), np.zeros((20, 4)), warm=0)
+    assert st & 4 and xo[0] == 2.1
+
+
+def test_qp_kkt_and_bounds(kp, cfgv):
+    N, M = 20, 2
+    x0 = _cold_instances(kp, cfgv, 2)
+    for b in range(2):
+        st, X, U, _ = ffi.prologue(kp, cfgv, N, M, x0[b], np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+        q = ffi.build_qp(kp, cfgv, N, M, X, U)
+        H = q["H"]
+        assert np.allclose(H, H.T, atol=1e-9 * np.abs(H).max())
+        assert np.linalg.eigvalsh(H).min() > 0
+        w, kkt = ffi.qp_solve(H, q["h"], q["lb"], q["ub"], q["C"], q["c"], 30)
+        assert kkt < 1e-9
+        assert np.all(w >= q["lb"] - 1e-9) and np.all(w <= q["ub"] + 1e-9)
+        assert np.all(q["C"] @ w >= q["c"] - 1e-8)
+
+
+def test_rti_closed_loop_is_stable(kp, cfgv):
+    N, M, K, B = 20, 2, 16, 8
+    x = _cold_instances(kp, cfgv, B)
+    X = np.zeros((B, N + 1, 15)); U = np.zeros((B, N, 4))
+    for step in range(12):
+        u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, X, U, warm=int(step > 0))
+        assert np.all(np.isfinite(diag)) and not np.any(st & 1)
+        assert np.all(diag[:, 5] < 1e-8)           # QP converged within K
+        assert np.all(u0 >= np.array([0.1, -0.1222, -0.1222, -5]) - 1e-6)
+        x = X[:, 1, :].copy()                       # nominal closed loop
+    # the RTI converged iterate is a fixed point of the step (no change when
+    # re-solved at the same initial state without shift)
+
+
+def test_rti_is_deterministic_and_batch_invariant(kp, cfgv):
+    N, M, K = 20, 2, 16
+    x = _cold_instances(kp, cfgv, 6)
+    X1 = np.zeros((6, N + 1, 15)); U1 = np.zeros((6, N, 4))
+    u1, d1, s1 = ffi.rti_step(kp, cfgv, N, M, K, x, X1, U1, warm=0, nthreads=4)
+    X2 = np.zeros((2, N + 1, 15)); U2 = np.zeros((2, N, 4))
+    u2, d2, s2 = ffi.rti_step(kp, cfgv, N, M, K, x[3:5].copy(), X2, U2, warm=0, nthreads=1)
+    np.testing.assert_array_equal(u1[3:5], u2)
+    np.testing.assert_array_equal(X1[3:5], X2)
