@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--substeps", type=int, default=2)
     ap.add_argument("--qp-iters", type=int, default=16)
+    ap.add_argument("--qp-kernel", type=int, default=0, help="0 auto, 1 wave-scalar, 2 MFMA-tiled")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
@@ -120,6 +121,7 @@ def main():
 
     B, N = args.batch, args.horizon
     cfg = ok.default_config(N=N, M=args.substeps, qp_iters=args.qp_iters, device=local)
+    cfg.qp_kernel = args.qp_kernel
     ctx = ok.BatchNMPC(ok.load_properties(), cfg, B)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)

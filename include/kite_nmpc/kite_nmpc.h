@@ -83,7 +83,9 @@ typedef struct kite_nmpc_config {
     int32_t shift;        /* 1: shift the warm start by one interval per step  */
     int32_t device;       /* HIP device ordinal                                 */
     int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
-    int32_t reserved[2];
+    int32_t qp_kernel;    /* 0: auto (MFMA-tiled QP when N == 20), 1: wave-scalar LDS QP,
+                             2: MFMA-tiled (KITE_EINVAL unless N == 20) */
+    int32_t reserved;
     double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
     double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */
     double R[4];          /* control weights (kiteNMPF.cpp:33)                 */

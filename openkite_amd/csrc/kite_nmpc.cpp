@@ -39,6 +39,9 @@ struct kite_nmpc_ctx {
     double *u0 = nullptr, *diag = nullptr, *kkt = nullptr;
     int32_t* status = nullptr;
     int32_t* iters = nullptr;
+    // tiled-QP layout (N == 20): H_aa tiles [B][15][4][64], H_ab [B][80][2], H_bb [B][2][2]
+    bool tiled = false;
+    double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     // scratch for the model-level entry points
     double* scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -130,6 +133,7 @@ int validate_config(const kite_nmpc_config& c) {
     for (int i = 0; i < 3; ++i) if (!(c.Q[i] >= 0.0)) return KITE_EINVAL;
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
+    if (c.qp_kernel < 0 || c.qp_kernel > 2) return KITE_EINVAL;
     return KITE_OK;
 }
 
@@ -156,7 +160,7 @@ int ensure_scratch(kite_nmpc_ctx* ctx, size_t bytes) {
 void free_ctx(kite_nmpc_ctx* ctx) {
     double** bufs[] = {&ctx->X, &ctx->U, &ctx->x0, &ctx->AB, &ctx->DEF, &ctx->Hs, &ctx->hs,
                        &ctx->Cr, &ctx->cl, &ctx->cu, &ctx->hmax, &ctx->u0, &ctx->diag, &ctx->kkt,
-                       &ctx->scratch};
+                       &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb};
     for (double** p : bufs) if (*p) { (void)hipFree(*p); *p = nullptr; }
     if (ctx->status) { (void)hipFree(ctx->status); ctx->status = nullptr; }
     if (ctx->iters) { (void)hipFree(ctx->iters); ctx->iters = nullptr; }
@@ -180,10 +184,16 @@ int run_step(kite_nmpc_ctx* ctx) {
     HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, s));
     if (ev) HIP_TRY(hipEventRecord(ev[2], s));
     HIP_TRY(kite::launch_condense(ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, ctx->Hs, ctx->hs, ctx->Cr,
-                                  ctx->cl, ctx->cu, ctx->hmax, s));
+                                  ctx->cl, ctx->cu, ctx->hmax, ctx->tiled ? 1 : 0, ctx->Htl, ctx->Hab, ctx->Hbb,
+                                  s));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
-    HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
-                            ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters, s));
+    if (ctx->tiled)
+        HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
+                                      ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
+                                      ctx->status, ctx->kkt, ctx->iters, s));
+    else
+        HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
+                                ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters, s));
     if (ev) HIP_TRY(hipEventRecord(ev[4], s));
     ctx->timed_step = (ev == ctx->ev);
     ctx->warm = true;
@@ -335,12 +345,18 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     ctx->mc = make_model_const(*params);
     ctx->rc = make_rti_const(*cfg);
     const size_t B = (size_t)batch, N = (size_t)cfg->N, n = 4 * N + 2;
+    const bool tiled_ok = kite::qp_tiled_supported(ctx->rc);
+    if (cfg->qp_kernel == 2 && !tiled_ok) { delete ctx; return KITE_EINVAL; }
+    ctx->tiled = cfg->qp_kernel == 2 || (cfg->qp_kernel == 0 && tiled_ok);
+    const size_t na = 4 * N;
     struct Alloc { double** p; size_t count; };
     const Alloc allocs[] = {
         {&ctx->X, B * (N + 1) * 15}, {&ctx->U, B * N * 4}, {&ctx->x0, B * 15},
-        {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13}, {&ctx->Hs, B * n * n},
+        {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13}, {&ctx->Hs, ctx->tiled ? 1 : B * n * n},
         {&ctx->hs, B * n}, {&ctx->Cr, B * N * n}, {&ctx->cl, B * N}, {&ctx->cu, B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
+        {&ctx->Htl, ctx->tiled ? B * 15 * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
+        {&ctx->Hbb, ctx->tiled ? B * 4 : 1},
     };
     for (const Alloc& a : allocs) {
         if (hipMalloc(a.p, a.count * sizeof(double)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
@@ -626,7 +642,32 @@ int kite_nmpc_get_qp(kite_nmpc_ctx* ctx, int32_t instance, double* H, double* h,
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t N = ctx->cfg.N, n = 4 * N + 2, b = instance;
     hipStream_t s = ctx->stream;
-    if (H) HIP_TRY(hipMemcpyAsync(H, ctx->Hs + b * n * n, n * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (H && !ctx->tiled)
+        HIP_TRY(hipMemcpyAsync(H, ctx->Hs + b * n * n, n * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (H && ctx->tiled) {
+        // reassemble the full matrix from the C-layout tiles (lane l: column l&15,
+        // rows (l>>4) + 4r), H_ab and H_bb
+        const size_t na = 4 * N;
+        std::vector<double> tl(15 * 256), ab(na * 2), bb(4);
+        HIP_TRY(hipMemcpyAsync(tl.data(), ctx->Htl + b * 15 * 256, tl.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ab.data(), ctx->Hab + b * na * 2, ab.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(bb.data(), ctx->Hbb + b * 4, 4 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        int t = 0;
+        for (int I = 0; I < 5; ++I)
+            for (int J = 0; J <= I; ++J, ++t)
+                for (int r = 0; r < 4; ++r)
+                    for (int l = 0; l < 64; ++l) {
+                        const size_t gi = 16 * I + (l >> 4) + 4 * r, gj = 16 * J + (l & 15);
+                        const double v = tl[(size_t)t * 256 + r * 64 + l];
+                        H[gi * n + gj] = v;
+                        H[gj * n + gi] = v;
+                    }
+        for (size_t i = 0; i < na; ++i)
+            for (size_t c = 0; c < 2; ++c) { H[i * n + na + c] = ab[i * 2 + c]; H[(na + c) * n + i] = ab[i * 2 + c]; }
+        for (size_t c = 0; c < 2; ++c)
+            for (size_t d = 0; d < 2; ++d) H[(na + c) * n + na + d] = bb[c * 2 + d];
+    }
     if (h) HIP_TRY(hipMemcpyAsync(h, ctx->hs + b * n, n * sizeof(double), hipMemcpyDeviceToHost, s));
     if (C) HIP_TRY(hipMemcpyAsync(C, ctx->Cr + b * N * n, N * n * sizeof(double), hipMemcpyDeviceToHost, s));
     if (cl) HIP_TRY(hipMemcpyAsync(cl, ctx->cl + b * N, N * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -229,6 +229,8 @@ __global__ __launch_bounds__(RK_T, 2) void k_rk4_sens(ModelConst P, int B, int N
 constexpr int NP = 96;          // padded QP dimension (6 tiles of 16)
 constexpr int WLD = 112;        // LDS row stride of the W chunk (doubles): 2*WLD % 64 == 32
 constexpr int NTILE = 21;       // lower-triangular 16x16 tiles of 96x96
+constexpr int QP_NTA = 5;       // tiled QP: control block 4N = 80 = 5 tiles (N = 20)
+constexpr int QP_NTILE = QP_NTA * (QP_NTA + 1) / 2;   // 15 lower tiles
 
 typedef double double4v __attribute__((ext_vector_type(4)));
 
@@ -258,7 +260,9 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
                                                  const double* __restrict__ DEF,
                                                  double* __restrict__ Hs, double* __restrict__ hs,
                                                  double* __restrict__ Cr, double* __restrict__ cl,
-                                                 double* __restrict__ cu, double* __restrict__ hmax) {
+                                                 double* __restrict__ cu, double* __restrict__ hmax, int tiled,
+                                                 double* __restrict__ Htl, double* __restrict__ Hab,
+                                                 double* __restrict__ Hbb) {
     __shared__ double sA[NK * 16 + NK + 3];
     __shared__ double Wc[16 * WLD];
     const int b = blockIdx.x;
@@ -285,17 +289,15 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
 
     // software prefetch of interval data (221 doubles -> <= 4 per lane)
     double pf[4];
-    auto load_interval = [&](int k) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = l + 64 * q;
-            double val = 0.0;
-            if (e < NK * 16) val = ABb[(size_t)k * NK * 16 + e];
-            else if (e < NK * 16 + NK) val = DEFb[(size_t)k * NK + (e - NK * 16)];
-            pf[q] = val;
-        }
-    };
-    if (N > 0) load_interval(0);
+#define KITE_LOAD_INTERVAL(k)                                                              \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                        \
+        const int e = l + 64 * q;                                                          \
+        double val = 0.0;                                                                  \
+        if (e < NK * 16) val = ABb[(size_t)(k) * NK * 16 + e];                             \
+        else if (e < NK * 16 + NK) val = DEFb[(size_t)(k) * NK + (e - NK * 16)];           \
+        pf[q] = val;                                                                       \
+    }
+    if (N > 0) { KITE_LOAD_INTERVAL(0) }
     __syncthreads();
 
     for (int k = 0; k <= N; ++k) {
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
             if (e < NK * 16 + NK) sA[e] = pf[q];
         }
         __syncthreads();
-        if (k + 1 < N) load_interval(k + 1);
+        if (k + 1 < N) { KITE_LOAD_INTERVAL(k + 1) }
         if ((kite_lane && k >= kb) || aff_lane) {
             double nv[NK];
             if (kite_lane && k == kb) {
@@ -409,32 +411,61 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
         __syncthreads();
     }
 
-    // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar)
+    // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar).
+    // tiled != 0 (k_qp_tiled): the control block H_aa (na = 4N = 16*NTA) goes
+    // out as C-layout tiles in lane order [tile][reg][lane], the theta
+    // couplings as H_ab [na][2] and H_bb [2][2]; otherwise the full n x n H.
     double* Hb = Hs + (size_t)b * n * n;
+    const int na = 4 * N;
     double lmax = 0.0;
-    int t = 0;
+    // scaled value of accumulator element (tile (I,J), reg r) or NaN if outside n x n
+    auto hval = [&](int I, int J, int r, double a, int& gi, int& gj) -> double {
+        gi = 16 * I + (l >> 4) + 4 * r;
+        gj = 16 * J + (l & 15);
+        double hv = a;
+        if (gi == gj) hv += col_rdiag(C, gi);
+        return hv * col_scale(C, gi) * col_scale(C, gj);
+    };
+    if (tiled) {
 #pragma unroll
-    for (int I = 0; I < 6; ++I) {
+        for (int I = 0; I < 6; ++I)
 #pragma unroll
-        for (int J = 0; J <= I; ++J) {
+            for (int J = 0; J <= I; ++J)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gi = 16 * I + (l >> 4) + 4 * r;
-                const int gj = 16 * J + (l & 15);
-                const double a = acc[t][r];
-                if (gi < n && gj < n) {
-                    double hv = a;
-                    if (gi == gj) hv += col_rdiag(C, gi);
-                    hv *= col_scale(C, gi) * col_scale(C, gj);
-                    Hb[(size_t)gi * n + gj] = hv;
-                    Hb[(size_t)gj * n + gi] = hv;
-                    lmax = fmax(lmax, fabs(hv));
-                } else if (gi == n && gj < n) {
-                    hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
+                for (int r = 0; r < 4; ++r) {
+                    int gi, gj;
+                    const double a = acc[I * (I + 1) / 2 + J][r];
+                    const double hv = hval(I, J, r, a, gi, gj);
+                    if (gi < n && gj < n) {
+                        if (gi < na) Htl[((size_t)b * QP_NTILE + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
+                        else if (gj < na) Hab[((size_t)b * na + gj) * 2 + (gi - na)] = hv;
+                        else {
+                            Hbb[(size_t)b * 4 + (gi - na) * 2 + (gj - na)] = hv;
+                            Hbb[(size_t)b * 4 + (gj - na) * 2 + (gi - na)] = hv;
+                        }
+                        lmax = fmax(lmax, fabs(hv));
+                    } else if (gi == n && gj < n) {
+                        hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
+                    }
                 }
-            }
-            ++t;
-        }
+    } else {
+#pragma unroll
+        for (int I = 0; I < 6; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    int gi, gj;
+                    const double a = acc[I * (I + 1) / 2 + J][r];
+                    const double hv = hval(I, J, r, a, gi, gj);
+                    if (gi < n && gj < n) {
+                        Hb[(size_t)gi * n + gj] = hv;
+                        Hb[(size_t)gj * n + gi] = hv;
+                        lmax = fmax(lmax, fabs(hv));
+                    } else if (gi == n && gj < n) {
+                        hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
+                    }
+                }
     }
     lmax = wave_max(lmax);
     if (l == 0) hmax[b] = lmax;
@@ -449,6 +480,115 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
 // (kiteNMPF.cpp:319-355) and status.
 // The normal matrix is factored in LDS (packed lower triangle).
 // ---------------------------------------------------------------------------
+// Expansion dx_{k+1} = A_k dx_k + B_k du_k + d_k (theta rows exact), trajectory
+// and control update, diagnostics (kiteNMPF.cpp:319-355) and status.  One
+// wavefront; w = scaled QP step in slots (i = l + 64 s); vec/col: LDS scratch.
+__device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[2], double kkt, int iters,
+                             const double* __restrict__ AB, const double* __restrict__ DEF,
+                             double* __restrict__ Xb, double* __restrict__ Ub, double* __restrict__ u0_out,
+                             double* __restrict__ diag, int32_t* __restrict__ status,
+                             double* __restrict__ kkt_out, int32_t* __restrict__ iters_out,
+                             double* vec, double* col) {
+    const int N = C.N, n = C.n;
+    // ---- expansion and trajectory update ------------------------------------
+    // physical step dw = D w_s into vec
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int i = l + 64 * s;
+        if (i < n) vec[i] = w[s] * col_scale(C, i);
+    }
+    __syncthreads();
+    const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
+    // theta / thetadot rows (exact double integrator), lane = node
+    for (int k = l; k <= N; k += 64) {
+        double dth = dth0 + (double)k * C.dt * dthd0, dthd = dthd0;
+        for (int m = 0; m < k; ++m) {
+            const double du = vec[3 * N + m];
+            dth += C.dt * C.dt * ((double)(k - m) - 0.5) * du;
+            dthd += C.dt * du;
+        }
+        Xb[k * NX + 13] += dth;
+        Xb[k * NX + 14] += dthd;
+    }
+    // controls
+    for (int e = l; e < N * NU; e += 64) {
+        const int k = e / NU, c = e % NU;
+        Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
+    }
+    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row)
+    {
+        double dx = 0.0;
+        const double* ABb = AB + (size_t)b * N * NK * 16;
+        const double* DEFb = DEF + (size_t)b * N * NK;
+        for (int k = 0; k < N; ++k) {
+            __syncthreads();
+            if (l < NK) col[l] = dx;
+            __syncthreads();
+            if (l < NK) {
+                const double* ar = ABb + ((size_t)k * NK + l) * 16;
+                double t = DEFb[(size_t)k * NK + l];
+                for (int j = 0; j < NK; ++j) t = fma(ar[j], col[j], t);
+                for (int c = 0; c < 3; ++c) t = fma(ar[NK + c], vec[3 * k + c], t);
+                dx = t;
+                Xb[(k + 1) * NX + l] += dx;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- diagnostics, cost, status -------------------------------------------
+    double cost = 0.0;
+    int bad = 0, bound = 0;
+    for (int k = l; k <= N; k += 64) {
+        const double* xk = Xb + k * NX;
+        double Pp[3], dP[3];
+        path_eval(C, xk[13], Pp, dP);
+        const bool last = (k == N);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double r = (last ? C.sqQ_T[a] : C.sqQ_dt[a]) * C.Sr[a] * (Pp[a] - xk[6 + a]);
+            cost += r * r;
+        }
+        if (!last) {
+            const double rv = C.sw * (C.sv * C.vref - C.sv * xk[14]);
+            cost += rv * rv;
+            for (int c = 0; c < NU; ++c) {
+                const double su = C.Su[c] * Ub[k * NU + c];
+                cost += C.dt * C.Rraw[c] * su * su;
+            }
+        }
+        for (int i = 0; i < NX; ++i) if (!isfinite(xk[i])) bad = 1;
+        if (k < N) for (int c = 0; c < NU; ++c) if (!isfinite(Ub[k * NU + c])) bad = 1;
+        if (k >= 1)
+            for (int i = 1; i < 13; ++i) if (xk[i] < C.lbx[i] || xk[i] > C.ubx[i]) bound = 1;
+    }
+    cost = wave_sum(cost);
+    bad = wave_or(bad);
+    bound = wave_or(bound);
+    if (l == 0) {
+        double Pp[3], dP[3];
+        path_eval(C, Xb[13], Pp, dP);
+        double pe = 0.0;
+        for (int a = 0; a < 3; ++a) { const double e = C.Sr[a] * (Pp[a] - Xb[6 + a]); pe += e * e; }
+        double* dg = diag + (size_t)b * 6;
+        dg[0] = sqrt(pe);
+        dg[1] = fabs(C.sv * C.vref - C.sv * Xb[14]);
+        dg[2] = cost;
+        dg[3] = Xb[13];
+        dg[4] = Ub[3];
+        dg[5] = kkt;
+        int32_t st = status[b];
+        if (bad) st |= 1;
+        if (!(kkt < 1e-8)) st |= 2;
+        if (bound && !bad) st |= 8;
+        status[b] = st;
+        if (kkt_out) kkt_out[b] = kkt;
+        if (iters_out) iters_out[b] = iters;
+        for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
+    }
+}
+
 constexpr int NMAX = 4 * KITE_NMAX + 2;                 // 82
 constexpr int NPACK = NMAX * (NMAX + 1) / 2;             // 3403
 constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
@@ -813,103 +953,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     residuals();
     const double kkt = resid;
 
-    // ---- expansion and trajectory update ------------------------------------
-    // physical step dw = D w_s into vec
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const int i = l + 64 * s;
-        if (i < n) vec[i] = q.w[s] * col_scale(C, i);
-    }
-    __syncthreads();
-    const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
-    // theta / thetadot rows (exact double integrator), lane = node
-    for (int k = l; k <= N; k += 64) {
-        double dth = dth0 + (double)k * C.dt * dthd0, dthd = dthd0;
-        for (int m = 0; m < k; ++m) {
-            const double du = vec[3 * N + m];
-            dth += C.dt * C.dt * ((double)(k - m) - 0.5) * du;
-            dthd += C.dt * du;
-        }
-        Xb[k * NX + 13] += dth;
-        Xb[k * NX + 14] += dthd;
-    }
-    // controls
-    for (int e = l; e < N * NU; e += 64) {
-        const int k = e / NU, c = e % NU;
-        Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
-    }
-    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row)
-    {
-        double dx = 0.0;
-        const double* ABb = AB + (size_t)b * N * NK * 16;
-        const double* DEFb = DEF + (size_t)b * N * NK;
-        for (int k = 0; k < N; ++k) {
-            __syncthreads();
-            if (l < NK) col[l] = dx;
-            __syncthreads();
-            if (l < NK) {
-                const double* ar = ABb + ((size_t)k * NK + l) * 16;
-                double t = DEFb[(size_t)k * NK + l];
-                for (int j = 0; j < NK; ++j) t = fma(ar[j], col[j], t);
-                for (int c = 0; c < 3; ++c) t = fma(ar[NK + c], vec[3 * k + c], t);
-                dx = t;
-                Xb[(k + 1) * NX + l] += dx;
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- diagnostics, cost, status -------------------------------------------
-    double cost = 0.0;
-    int bad = 0, bound = 0;
-    for (int k = l; k <= N; k += 64) {
-        const double* xk = Xb + k * NX;
-        double Pp[3], dP[3];
-        path_eval(C, xk[13], Pp, dP);
-        const bool last = (k == N);
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const double r = (last ? C.sqQ_T[a] : C.sqQ_dt[a]) * C.Sr[a] * (Pp[a] - xk[6 + a]);
-            cost += r * r;
-        }
-        if (!last) {
-            const double rv = C.sw * (C.sv * C.vref - C.sv * xk[14]);
-            cost += rv * rv;
-            for (int c = 0; c < NU; ++c) {
-                const double su = C.Su[c] * Ub[k * NU + c];
-                cost += C.dt * C.Rraw[c] * su * su;
-            }
-        }
-        for (int i = 0; i < NX; ++i) if (!isfinite(xk[i])) bad = 1;
-        if (k < N) for (int c = 0; c < NU; ++c) if (!isfinite(Ub[k * NU + c])) bad = 1;
-        if (k >= 1)
-            for (int i = 1; i < 13; ++i) if (xk[i] < C.lbx[i] || xk[i] > C.ubx[i]) bound = 1;
-    }
-    cost = wave_sum(cost);
-    bad = wave_or(bad);
-    bound = wave_or(bound);
-    if (l == 0) {
-        double Pp[3], dP[3];
-        path_eval(C, Xb[13], Pp, dP);
-        double pe = 0.0;
-        for (int a = 0; a < 3; ++a) { const double e = C.Sr[a] * (Pp[a] - Xb[6 + a]); pe += e * e; }
-        double* dg = diag + (size_t)b * 6;
-        dg[0] = sqrt(pe);
-        dg[1] = fabs(C.sv * C.vref - C.sv * Xb[14]);
-        dg[2] = cost;
-        dg[3] = Xb[13];
-        dg[4] = Ub[3];
-        dg[5] = kkt;
-        int32_t st = status[b];
-        if (bad) st |= 1;
-        if (!(kkt < 1e-8)) st |= 2;
-        if (bound && !bad) st |= 8;
-        status[b] = st;
-        if (kkt_out) kkt_out[b] = kkt;
-        if (iters_out) iters_out[b] = iters;
-        for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
-    }
+    rti_epilogue(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out, vec, col);
 }
 
 // ---------------------------------------------------------------------------
@@ -1040,8 +1084,9 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
 }
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
                            const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
-                           double* hmax, hipStream_t s) {
-    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), 0, s, C, B, X, U, AB, DEF, Hs, hs, Cr, cl, cu, hmax);
+                           double* hmax, int tiled, double* Htl, double* Hab, double* Hbb, hipStream_t s) {
+    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), 0, s, C, B, X, U, AB, DEF, Hs, hs, Cr, cl, cu, hmax,
+                       tiled, Htl, Hab, Hbb);
     return hipGetLastError();
 }
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
@@ -1077,5 +1122,7 @@ hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos,
     hipLaunchKernelGGL(k_closest_point, dim3((count + 63) / 64), dim3(64), 0, s, C, count, pos, guess, theta);
     return hipGetLastError();
 }
+
+#include "qp_tiled.inc"
 
 }  // namespace kite

@@ -38,7 +38,14 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
                            double* AB, double* DEF, hipStream_t s);
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
                            const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
-                           double* hmax, hipStream_t s);
+                           double* hmax, int tiled, double* Htl, double* Hab, double* Hbb, hipStream_t s);
+// Tiled-QP path (N == 20): H_aa as 15 lower 16x16 C-layout tiles in lane order.
+bool qp_tiled_supported(const RtiConst& C);
+hipError_t launch_qp_tiled(const ModelConst& P, const RtiConst& C, int B, const double* Htl, const double* Hab,
+                           const double* Hbb, const double* hs, const double* Cr, const double* cl,
+                           const double* cu, const double* hmax, const double* AB, const double* DEF, double* X,
+                           double* U, double* u0, double* diag, int32_t* status, double* kkt, int32_t* iters,
+                           hipStream_t s);
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
