@@ -135,8 +135,12 @@ int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* 
 int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref);
 /* disableWarmStart (kiteNMPF.h:40): the next step cold-starts.              */
 int kite_nmpc_reset(kite_nmpc_ctx* ctx);
-/* Run on this HIP stream (hipStream_t as void*; NULL = the context's own).  */
+/* Run on this HIP stream (hipStream_t as void*).  NULL is the HIP null
+ * (legacy default) stream -- the stream PyTorch's default stream maps to.
+ * A new context runs on a private non-blocking stream; restore it with
+ * kite_nmpc_use_own_stream.                                                  */
 int kite_nmpc_set_stream(kite_nmpc_ctx* ctx, void* hip_stream);
+int kite_nmpc_use_own_stream(kite_nmpc_ctx* ctx);
 int kite_nmpc_synchronize(kite_nmpc_ctx* ctx);
 
 /* findClosestPointOnPath (kiteNMPF.cpp:358-391), batched over `count`

@@ -417,7 +417,13 @@ int kite_nmpc_reset(kite_nmpc_ctx* ctx) {
 
 int kite_nmpc_set_stream(kite_nmpc_ctx* ctx, void* hip_stream) {
     if (!ctx) return KITE_EINVAL;
-    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    ctx->stream = (hipStream_t)hip_stream;
+    return KITE_OK;
+}
+
+int kite_nmpc_use_own_stream(kite_nmpc_ctx* ctx) {
+    if (!ctx) return KITE_EINVAL;
+    ctx->stream = ctx->own_stream;
     return KITE_OK;
 }
 

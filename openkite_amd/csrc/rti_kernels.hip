@@ -41,6 +41,14 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
+// NaN-propagating max (fmax drops NaN: a poisoned KKT residual must never
+// read as converged)
+__device__ __forceinline__ double nmax(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
+__device__ __forceinline__ double wave_nmax(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
@@ -737,8 +745,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                 q.rd[s] = hw[s] + q.h[s] - (q.zl[s] - q.zu[s]) - ctz[s];
                 q.rpl[s] = q.w[s] - q.lb[s] - q.sl[s];
                 q.rpu[s] = q.ub[s] - q.w[s] - q.su[s];
-                rmax = fmax(rmax, fabs(q.rd[s]) * dscale);
-                rmax = fmax(rmax, fmax(fabs(q.rpl[s]), fabs(q.rpu[s])));
+                rmax = nmax(rmax, fabs(q.rd[s]) * dscale);
+                rmax = nmax(rmax, fmax(fabs(q.rpl[s]), fabs(q.rpu[s])));
                 mu += q.sl[s] * q.zl[s] + q.su[s] * q.zu[s];
             } else {
                 q.rd[s] = 0.0; q.rpl[s] = 0.0; q.rpu[s] = 0.0;
@@ -746,12 +754,12 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         }
         q.rplo = 0.0; q.rphi = 0.0;
         if (row_lane) {
-            if (has_lo) { q.rplo = q.cw - q.clo - q.slo; rmax = fmax(rmax, fabs(q.rplo)); mu += q.slo * q.zlo; }
-            if (has_hi) { q.rphi = q.chi - q.cw - q.shi; rmax = fmax(rmax, fabs(q.rphi)); mu += q.shi * q.zhi; }
+            if (has_lo) { q.rplo = q.cw - q.clo - q.slo; rmax = nmax(rmax, fabs(q.rplo)); mu += q.slo * q.zlo; }
+            if (has_hi) { q.rphi = q.chi - q.cw - q.shi; rmax = nmax(rmax, fabs(q.rphi)); mu += q.shi * q.zhi; }
         }
-        rmax = wave_max(rmax);
+        rmax = wave_nmax(rmax);
         mu = wave_sum(mu) / (double)nI;
-        resid = fmax(rmax, mu);
+        resid = nmax(rmax, mu);
         return mu;
     };
 
@@ -877,7 +885,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     int iters = C.K;
     for (int it = 0; it < C.K; ++it) {
         const double mu = residuals();
-        if (resid < IPM_FREEZE) { iters = it; break; }
+        if (resid < IPM_FREEZE || resid != resid) { iters = it; break; }   // converged, or poisoned
         // sigma = z/s and the normal matrix H + A' Sigma A into Lp
 #pragma unroll
         for (int s = 0; s < 2; ++s) {

@@ -88,6 +88,7 @@ _SIGNATURES = {
     "kite_nmpc_set_reference_velocity": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     "kite_nmpc_reset": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "kite_nmpc_use_own_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_closest_point": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP]),
     "kite_nmpc_step": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, ctypes.POINTER(MpcDiagnostic), _IP]),
@@ -123,6 +124,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C openkite_amd/csrc` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
+        # One HIP runtime per process.  PyTorch-ROCm ships its own
+        # libamdhip64 (SONAME libamdhip64.so.7) and NEEDs it by the unversioned
+        # name: if /opt/rocm's copy is mapped first, torch maps a second one
+        # and sees no GPU (and torch stream handles mean nothing to ours).
+        # Mapping torch first makes our NEEDED libamdhip64.so.7 bind to it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
             fn = getattr(L, name)
@@ -213,8 +223,13 @@ class BatchNMPC:
         _check(lib().kite_nmpc_reset(self._h), "reset")
 
     def set_stream(self, stream_ptr: int):
+        """Run on this hipStream_t (int handle; 0 = the HIP null stream, which is
+        torch's default stream)."""
         _check(lib().kite_nmpc_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None),
                "set_stream")
+
+    def use_own_stream(self):
+        _check(lib().kite_nmpc_use_own_stream(self._h), "use_own_stream")
 
     def synchronize(self):
         _check(lib().kite_nmpc_synchronize(self._h), "synchronize")

@@ -217,6 +217,36 @@ def test_qp_kernels_vs_oracle(kp, cfgv, qp_kernel):
         g.close()
 
 
+def test_step_device_on_torch_stream_matches_host_step():
+    """Device-pointer entry point on torch's default stream (handle 0 = HIP null
+    stream), closed loop on the device, bitwise equal to the host entry point."""
+    torch = pytest.importorskip("torch")
+    B = 64
+    x0 = x0_batch(B, offset=3000)
+    cfg = ok.default_config()
+    gh = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    gd = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    try:
+        gd.set_stream(torch.cuda.current_stream().cuda_stream)
+        d_x0 = torch.from_numpy(x0.copy()).cuda()
+        d_u0 = torch.zeros((B, 4), dtype=torch.float64, device="cuda")
+        d_tr = torch.zeros((B, N + 1, 15), dtype=torch.float64, device="cuda")
+        d_dg = torch.zeros((B, 6), dtype=torch.float64, device="cuda")
+        d_st = torch.zeros((B,), dtype=torch.int32, device="cuda")
+        x = x0.copy()
+        for step in range(4):
+            r = gh.step(x)
+            x = r["traj"][:, 1, :].copy()
+            gd.step_device(d_x0.data_ptr(), d_u0.data_ptr(), d_tr.data_ptr(), 0, d_dg.data_ptr(), d_st.data_ptr())
+            d_x0.copy_(d_tr[:, 1, :])          # torch op on the same stream, no host sync
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d_u0.cpu().numpy(), r["u0"])
+        np.testing.assert_array_equal(d_tr.cpu().numpy(), r["traj"])
+        np.testing.assert_array_equal(d_st.cpu().numpy(), r["status"])
+    finally:
+        gh.close(); gd.close()
+
+
 def test_kite_nmpf_facade_reference_order():
     """KiteNMPF mirror: last column of getOptimalControl() is u(t0) (nmpf_node.cpp:124)."""
     nm = ok.KiteNMPF()
