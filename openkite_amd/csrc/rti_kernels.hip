@@ -31,33 +31,77 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     hi = __builtin_amdgcn_readlane(hi, lane);
     return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---------------------------------------------------------------------------
+// cross-lane primitives, all VALU (no LDS round trip).  Lane semantics of the
+// gfx950 permlane swaps, probed on the device (tools/probes/lane_ops.hip):
+//   permlane16_swap(x, x) -> {rows [0,0,2,2], rows [1,1,3,3]}   (16-lane rows)
+//   permlane32_swap(x, x) -> {lanes [0-31, 0-31], lanes [32-63, 32-63]}
+//   DPP row_newbcast:p    -> lane p of each 16-lane row, to the whole row
+// All of these must be called in wave-uniform control flow.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// {value of rows [0,0,2,2], value of rows [1,1,3,3]}
+__device__ __forceinline__ void swap16_d(double v, double& ev, double& od) {
+    const auto L = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto H = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    ev = __hiloint2double((int)H[0], (int)L[0]);
+    od = __hiloint2double((int)H[1], (int)L[1]);
+}
+// {value of lanes [0-31, 0-31], value of lanes [32-63, 32-63]}
+__device__ __forceinline__ void swap32_d(double v, double& lo_half, double& hi_half) {
+    const auto L = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto H = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    lo_half = __hiloint2double((int)H[0], (int)L[0]);
+    hi_half = __hiloint2double((int)H[1], (int)L[1]);
+}
+// reduce over the 16 lanes of each row (every lane gets its row's result)
+template <class Op>
+__device__ __forceinline__ double row_reduce16(double v, Op op) {
+    v = op(v, dpp_d<0x128>(v));   // row_ror:8
+    v = op(v, dpp_d<0x124>(v));   // row_ror:4
+    v = op(v, dpp_d<0x122>(v));   // row_ror:2
+    v = op(v, dpp_d<0x121>(v));   // row_ror:1
     return v;
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+// reduce over the 4 lanes l, l^16, l^32, l^48 (same position in each row)
+template <class Op>
+__device__ __forceinline__ double col_reduce4(double v, Op op) {
+    double a, b;
+    swap16_d(v, a, b);
+    v = op(a, b);
+    swap32_d(v, a, b);
+    return op(a, b);
 }
+// value of row-group q (lanes 16q..16q+15), delivered to the same position of every row
+__device__ __forceinline__ double bcast_rowgroup(double v, int q) {
+    double a, b;
+    swap16_d(v, a, b);
+    const double t = (q & 1) ? b : a;
+    swap32_d(t, a, b);
+    return (q & 2) ? b : a;
+}
+struct OpAdd { __device__ double operator()(double a, double b) const { return a + b; } };
+struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
 // NaN-propagating max (fmax drops NaN: a poisoned KKT residual must never
 // read as converged)
 __device__ __forceinline__ double nmax(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
-__device__ __forceinline__ double wave_nmax(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
-}
+struct OpNMax { __device__ double operator()(double a, double b) const { return nmax(a, b); } };
+
+__device__ __forceinline__ double row_sum16(double v) { return row_reduce16(v, OpAdd()); }
+__device__ __forceinline__ double col_sum4(double v) { return col_reduce4(v, OpAdd()); }
+__device__ __forceinline__ double wave_sum(double v) { return col_reduce4(row_reduce16(v, OpAdd()), OpAdd()); }
+__device__ __forceinline__ double wave_max(double v) { return col_reduce4(row_reduce16(v, OpMax()), OpMax()); }
+__device__ __forceinline__ double wave_nmax(double v) { return col_reduce4(row_reduce16(v, OpNMax()), OpNMax()); }
+__device__ __forceinline__ double wave_min(double v) { return col_reduce4(row_reduce16(v, OpMin()), OpMin()); }
 __device__ __forceinline__ int wave_or(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-    return v;
+    // flags are 0/1: reuse the fp64 max path
+    return wave_max((double)v) != 0.0 ? 1 : 0;
 }
 
 // Path P(theta) = q_r^-1 (x) [0, R cos, R sin, alt] (x) q_r and dP/dtheta
@@ -600,6 +644,11 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
 constexpr int NMAX = 4 * KITE_NMAX + 2;                 // 82
 constexpr int NPACK = NMAX * (NMAX + 1) / 2;             // 3403
 constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
+// Cholesky pivot safeguard (Wright 1999, see oracle/kite_oracle.cpp chol): a
+// pivot <= 0 from rounding near convergence is replaced by a huge value,
+// freezing that direction for the step; NaN stays NaN.
+constexpr double KITE_PIV_BIG = 1e128;
+__device__ __forceinline__ double piv_fix(double s) { return s <= 0.0 ? KITE_PIV_BIG : s; }
 
 __device__ __forceinline__ int pk(int i, int c) { return (i * (i + 1)) / 2 + c; }
 
@@ -766,7 +815,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     // Cholesky of the packed matrix in Lp (in place, lower)
     auto cholesky = [&]() {
         for (int j = 0; j < n; ++j) {
-            const double piv = Lp[pk(j, j)];
+            const double piv = piv_fix(Lp[pk(j, j)]);
             const double dj = sqrt(piv);
             const double inv = 1.0 / dj;
             __syncthreads();

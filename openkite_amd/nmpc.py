@@ -17,7 +17,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkite_nmpc.so")
+LIB_PATH = os.environ.get("KITE_NMPC_LIB", os.path.join(_HERE, "lib", "libkite_nmpc.so"))
 REPO = os.path.dirname(_HERE)
 DEFAULT_PARAMS = os.path.join(REPO, "data", "umx_radian.yaml")
 

@@ -15,8 +15,11 @@ from oracle import ffi
 pytestmark = pytest.mark.gpu
 
 N, M, K = 20, 2, 16
-RTI_TOL = 1e-7      # RTI u0/traj/ctrl, relative to max(1,|oracle|) per array
-                    # (QP condition number ~1e11 in scaled variables: see DESIGN.md)
+RTI_TOL = 1e-6      # RTI u0/traj/ctrl, relative to max(1,|oracle|) per array.
+                    # cond(H) ~ 1e11 in the scaled QP variables: a 1e-15 relative
+                    # perturbation of H moves the ORACLE's own solution by up to
+                    # ~2.5e-7 (pinned by test_oracle.py::test_qp_sensitivity_envelope),
+                    # so two correct fp64 solvers agree only to that envelope.
 
 
 def rel(a, b):

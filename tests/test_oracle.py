@@ -189,3 +189,24 @@ def test_rti_is_deterministic_and_batch_invariant(kp, cfgv):
     u2, d2, s2 = ffi.rti_step(kp, cfgv, N, M, K, x[3:5].copy(), X2, U2, warm=0, nthreads=1)
     np.testing.assert_array_equal(u1[3:5], u2)
     np.testing.assert_array_equal(X1[3:5], X2)
+
+
+def test_qp_sensitivity_envelope(kp, cfgv):
+    """Intrinsic sensitivity of the condensed QP (justifies RTI_TOL in
+    test_gpu_parity.py): symmetric relative perturbations of H of 1e-15 --
+    rounding-level differences between two fp64 implementations -- move the
+    oracle's own QP solution by more than 1e-8 on some instance and by less
+    than 1e-6 on all of them (cold start, instances of test_qp_kernels_vs_oracle)."""
+    from tests.test_gpu_parity import x0_batch
+    N, M, K = 20, 2, 16
+    x = x0_batch(16, offset=2000)
+    worst = 0.0
+    for b in range(16):
+        st, X, U, _ = ffi.prologue(kp, cfgv, N, M, x[b], np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+        q = ffi.build_qp(kp, cfgv, N, M, X, U)
+        w0, k0 = ffi.qp_solve(q["H"], q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
+        E = np.random.default_rng(b).normal(size=q["H"].shape) * 1e-15
+        w1, k1 = ffi.qp_solve(q["H"] * (1 + (E + E.T) / 2), q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
+        assert k0 < 1e-8 and k1 < 1e-8
+        worst = max(worst, np.abs(w1 - w0).max() / max(1.0, np.abs(w0).max()))
+    assert 1e-8 < worst < 1e-6, worst

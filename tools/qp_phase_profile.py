@@ -1,0 +1,42 @@
+"""Phase profile of k_qp_tiled (s_memtime cycles per phase, mean per instance).
+
+Runs the phase-instrumented build (make -C openkite_amd/csrc prof) on one
+closed-loop bench-like workload.  Tools only: not part of the product path.
+"""
+import ctypes
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+os.environ["KITE_NMPC_LIB"] = os.path.join(REPO, "openkite_amd", "lib", "libkite_nmpc_prof.so")
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import openkite_amd as ok  # noqa: E402
+from tests.test_gpu_parity import x0_batch  # noqa: E402
+
+PHASES = ["init", "residual", "normal_matrix", "cholesky", "schur", "predictor", "corrector",
+          "final_residual", "epilogue"]
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+L = ok.lib()
+L.kite_debug_qp_profile.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+buf = (ctypes.c_ulonglong * 16)()
+g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), B)
+x = x0_batch(B)
+for step in range(4):
+    r = g.step(x)
+    x = r["traj"][:, 1, :].copy()
+L.kite_debug_qp_profile(buf)          # clear warm-up
+r = g.step(x)
+L.kite_debug_qp_profile(buf)
+v = np.array(buf[:16], dtype=np.float64)
+ninst, its = v[10], v[9]
+print(f"B={B} instances={ninst:.0f} mean iterations={its / ninst:.2f}")
+tot = v[:9].sum() / ninst
+for i, p in enumerate(PHASES):
+    c = v[i] / ninst
+    per_it = c / (its / ninst) if i in (1, 2, 3, 4, 5, 6) else float("nan")
+    print(f"{p:15s} {c:12.0f} cycles/instance  {100 * c / tot:5.1f}%  per-iteration {per_it:10.0f}")
+print(f"{'total':15s} {tot:12.0f}")
+g.close()
