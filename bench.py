@@ -102,6 +102,20 @@ def cpu_baseline(args, x0_host, budget_s):
                        f"K<={args.qp_iters}), oracle/kite_oracle.cpp -O3 OpenMP {threads} threads, {el:.1f} s")
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>_pmc_hbm.json, written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
+    for f in reversed(files):
+        d = json.load(open(f)).get("kernels", {})
+        for name in (f"k_{kernel}_tiled", f"k_{kernel}"):
+            if name in d and "traffic_bytes" in d[name]:
+                return d[name]["traffic_bytes"], os.path.relpath(f, ROOT) + f" ({name})"
+    return None, "no PMC summary"
+
+
 def main():
     args = parse()
     import torch
@@ -179,10 +193,12 @@ def main():
         dom_flops = fl.get(dom, 0.0) * B
         achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic(dom)
         roofline = dict(bound="mfma", achieved=round(achieved, 4), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=None, kernel=dom,
-                        note="fp64 compute roof (vector = matrix peak on gfx950); algorithmic flops "
-                             "per launch from openkite_amd/flops.py; traffic: see profiles/")
+                        frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic, kernel=dom,
+                        note="fp64 compute roof (vector = matrix peak on gfx950); achieved = algorithmic flops "
+                             "per launch (openkite_amd/flops.py) / mean launch time (HIP events on the step "
+                             f"stream); traffic = HBM bytes per launch from {tsrc}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, x0_host, args.cpu_seconds)

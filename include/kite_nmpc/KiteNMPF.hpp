@@ -1,0 +1,172 @@
+// KiteNMPF.hpp -- header-only C++ facade over the C ABI (kite_nmpc.h) with the
+// method names and semantics of the reference controller class
+// (src/kite_control/kiteNMPF.h:10-118) for ONE kite, so that the ROS node
+// (src/kite_control/nmpf_node.cpp) can switch with a one-line type change;
+// see INTEGRATION.md.  casadi::DM arguments become std::vector<double>
+// (matrices column-major, as DM stores them).
+//
+// Differences kept deliberately visible:
+//   * the OCP is fixed at createNLP() (an RTI context), setters before it
+//     configure, bound setters after it update the live context;
+//   * getOptimalControl()/getOptimalTrajetory() keep the reference's REVERSED
+//     time order (last column = t0, nmpf_node.cpp:124 reads column N);
+//   * getStats() returns the IPOPT-style return_status string only;
+//   * initialized() mirrors the reference, which never sets it (kiteNMPF.cpp:46).
+#pragma once
+
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kite_nmpc.h"
+
+namespace kite_amd {
+
+class KiteNmpcError : public std::runtime_error {
+public:
+    explicit KiteNmpcError(int code, const std::string& what)
+        : std::runtime_error(what + ": " + kite_nmpc_strerror(code)), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+inline void kite_check(int rc, const char* what) {
+    if (rc < 0) throw KiteNmpcError(rc, what);
+}
+
+// KiteDynamics stand-in: the parameter set (kite_utils::LoadProperties, kite.cpp:7-76)
+inline kite_params LoadProperties(const std::string& yaml_path) {
+    kite_params p;
+    kite_check(kite_params_load_yaml(yaml_path.c_str(), &p), "LoadProperties");
+    return p;
+}
+
+class KiteNMPF {
+public:
+    // KiteNMPF(shared_ptr<KiteDynamics>, path) (kiteNMPF.h:14): the dynamics are the
+    // parameter set, the path is the rotated circle of the config (nmpf_node.cpp:30-40)
+    explicit KiteNMPF(const kite_params& params, int N = 20, double dt = 0.05) : params_(params) {
+        kite_nmpc_default_config(&cfg_);
+        cfg_.N = N;
+        cfg_.dt = dt;
+    }
+    KiteNMPF(const kite_params& params, const kite_nmpc_config& cfg) : params_(params), cfg_(cfg) {}
+    ~KiteNMPF() { kite_nmpc_destroy(ctx_); }
+    KiteNMPF(const KiteNMPF&) = delete;
+    KiteNMPF& operator=(const KiteNMPF&) = delete;
+
+    // ---- setters (kiteNMPF.h:20-34) ----------------------------------------
+    void setLBX(const std::vector<double>& v) { set_bounds(cfg_.lbx, v, 15, "setLBX"); }
+    void setUBX(const std::vector<double>& v) { set_bounds(cfg_.ubx, v, 15, "setUBX"); }
+    void setLBU(const std::vector<double>& v) { set_bounds(cfg_.lbu, v, 4, "setLBU"); }
+    void setUBU(const std::vector<double>& v) { set_bounds(cfg_.ubu, v, 4, "setUBU"); }
+    void setLBG(const std::vector<double>&) {}   // collocation equality bounds: no RTI counterpart
+    void setUBG(const std::vector<double>&) {}
+    // 15x15 / 4x4 diagonal scaling matrices (column-major) or their diagonals
+    void setStateScaling(const std::vector<double>& S) { set_diag(cfg_.Sx, S, 15, "setStateScaling"); }
+    void setControlScaling(const std::vector<double>& S) { set_diag(cfg_.Su, S, 4, "setControlScaling"); }
+    // physical path speed (the reference stores Sx(14,14) * v, so it had to follow
+    // setStateScaling; stored physical here, order-independent)
+    void setReferenceVelocity(double v) {
+        cfg_.vref = v;
+        if (ctx_) kite_check(kite_nmpc_set_reference_velocity(ctx_, v), "setReferenceVelocity");
+    }
+
+    // ---- lifecycle (kiteNMPF.h:37-41) ---------------------------------------
+    void createNLP() {
+        kite_nmpc_destroy(ctx_);
+        ctx_ = nullptr;
+        kite_check(kite_nmpc_create(&params_, &cfg_, 1, &ctx_), "createNLP");
+        warm_ = false;
+    }
+    void enableWarmStart() { warm_ = true; }
+    void disableWarmStart() {
+        warm_ = false;
+        if (ctx_) kite_check(kite_nmpc_reset(ctx_), "disableWarmStart");
+    }
+    // one RTI step from the physical 15-state X0 (kiteNMPF.cpp:199-316)
+    void computeControl(const std::vector<double>& X0) {
+        if (X0.size() != 15) throw std::invalid_argument("computeControl: X0 must have 15 entries");
+        if (!ctx_) createNLP();
+        if (!warm_) kite_check(kite_nmpc_reset(ctx_), "computeControl");
+        const int N = cfg_.N;
+        traj_.assign((size_t)(N + 1) * 15, 0.0);
+        ctrl_.assign((size_t)N * 4, 0.0);
+        kite_check(kite_nmpc_step(ctx_, X0.data(), u0_, traj_.data(), ctrl_.data(), &diag_, &status_),
+                   "computeControl");
+        warm_ = true;
+    }
+
+    // ---- getters (kiteNMPF.h:42-60) -----------------------------------------
+    // 4 x N, column-major, reference column order: last column = u(t0)
+    std::vector<double> getOptimalControl() const {
+        const int N = cfg_.N;
+        std::vector<double> out((size_t)4 * N);
+        for (int k = 0; k < N; ++k)
+            for (int c = 0; c < 4; ++c) out[(size_t)(N - 1 - k) * 4 + c] = ctrl_.empty() ? 0.0 : ctrl_[k * 4 + c];
+        return out;
+    }
+    // 15 x (N+1), column-major, reference column order: last column = x(t0)
+    std::vector<double> getOptimalTrajetory() const {   // [sic] kiteNMPF.h:44
+        const int N = cfg_.N;
+        std::vector<double> out((size_t)15 * (N + 1));
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 15; ++i) out[(size_t)(N - k) * 15 + i] = traj_.empty() ? 0.0 : traj_[k * 15 + i];
+        return out;
+    }
+    // "return_status" of getStats() (kiteNMPF.cpp:303-313)
+    std::string getStats() const {
+        if (status_ & KITE_ST_NAN) return "Invalid_Number_Detected";
+        if (status_ & KITE_ST_QP_NOT_CONV) return "Maximum_Iterations_Exceeded";
+        return "Solve_Succeeded";
+    }
+    int32_t statusBits() const { return status_; }
+    double getPathError() const { return diag_.pos_error; }
+    double getVelocityError() const { return diag_.vel_error; }
+    double getVirtState() const { return diag_.virt_state; }
+    const kite_mpc_diagnostic& diagnostic() const { return diag_; }
+    // u(t0) = [T, dE, dR, Uv] (what nmpf_node.cpp:120-138 publishes)
+    const double* controlAtT0() const { return u0_; }
+    bool initialized() const { return false; }   // never set in the reference (kiteNMPF.cpp:46)
+    // findClosestPointOnPath (kiteNMPF.cpp:358-391)
+    double findClosestPointOnPath(const std::vector<double>& position, double init_guess = 0.0) {
+        if (position.size() != 3) throw std::invalid_argument("findClosestPointOnPath: 3 entries");
+        if (!ctx_) createNLP();
+        double th = 0.0;
+        kite_check(kite_nmpc_closest_point(ctx_, 1, position.data(), &init_guess, &th), "findClosestPointOnPath");
+        return th;
+    }
+    kite_nmpc_ctx* context() { return ctx_; }
+
+private:
+    void set_bounds(double* dst, const std::vector<double>& v, size_t n, const char* what) {
+        if (v.size() != n) throw std::invalid_argument(std::string(what) + ": wrong size");
+        std::memcpy(dst, v.data(), n * sizeof(double));
+        if (ctx_) kite_check(kite_nmpc_set_bounds(ctx_, cfg_.lbx, cfg_.ubx, cfg_.lbu, cfg_.ubu), what);
+    }
+    void set_diag(double* dst, const std::vector<double>& S, size_t n, const char* what) {
+        if (S.size() == n * n) {
+            for (size_t i = 0; i < n; ++i) dst[i] = S[i * n + i];
+        } else if (S.size() == n) {
+            std::memcpy(dst, S.data(), n * sizeof(double));
+        } else {
+            throw std::invalid_argument(std::string(what) + ": wrong size");
+        }
+        if (ctx_) createNLP();   // scaling is part of the OCP: rebuild (reference: before createNLP)
+    }
+
+    kite_params params_;
+    kite_nmpc_config cfg_;
+    kite_nmpc_ctx* ctx_ = nullptr;
+    bool warm_ = false;
+    std::vector<double> traj_, ctrl_;
+    double u0_[4] = {0, 0, 0, 0};
+    kite_mpc_diagnostic diag_{};
+    int32_t status_ = 0;
+};
+
+}  // namespace kite_amd

@@ -10,4 +10,4 @@ timeout -k 10 300 python bench.py --steps 30 --warmup 3 --cpu-seconds 10 --qp-ke
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --qp-kernel $QK > $OUT/prof_bench.log 2>&1 || { echo "rocprof failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o fetch --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o write --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
-echo done
+timeout -k 10 60 python tools/pmc_summary.py $OUT $TAG > $OUT/pmc_summary.log 2>&1 && cp profiles/${TAG}_* $OUT/ ; echo done
