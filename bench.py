@@ -122,6 +122,7 @@ def main():
     import torch.distributed as dist
     import openkite_amd as ok
     from openkite_amd import flops
+    from openkite_amd.shard import Publisher, max_over_ranks, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -140,22 +141,21 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
 
-    x0_host = synthetic_x0(B, rank * B, ctx)
+    offset, count = shard(world * B, world, rank)      # weak scaling: B instances per GPU
+    assert count == B
+    x0_host = synthetic_x0(B, offset, ctx)
     d_x0 = torch.from_numpy(x0_host).to(dev)
     d_u0 = torch.zeros((B, 4), dtype=torch.float64, device=dev)
     d_traj = torch.zeros((B, N + 1, 15), dtype=torch.float64, device=dev)
     d_diag = torch.zeros((B, 6), dtype=torch.float64, device=dev)
     d_status = torch.zeros((B,), dtype=torch.int32, device=dev)
-    d_pub = torch.zeros((B, 10), dtype=torch.float64, device=dev)
-    gather = torch.zeros((world * B, 10), dtype=torch.float64, device=dev) if world > 1 else None
+    pub = Publisher(B, dev, world) if world > 1 and not args.no_allgather else None
 
     def one_step():
         ctx.step_device(d_x0.data_ptr(), d_u0.data_ptr(), d_traj.data_ptr(), 0, d_diag.data_ptr(),
                         d_status.data_ptr())
-        if gather is not None and not args.no_allgather:
-            d_pub[:, :4].copy_(d_u0)
-            d_pub[:, 4:].copy_(d_diag)
-            dist.all_gather_into_tensor(gather, d_pub)
+        if pub is not None:
+            pub.publish(d_u0, d_diag)          # all ranks see every kite's u0 + diagnostics
         d_x0.copy_(d_traj[:, 1, :])        # closed loop: predicted state at t0 + dt
 
     for _ in range(args.warmup):
@@ -177,10 +177,7 @@ def main():
     kkt, iters = ctx.qp_stats()
     status = d_status.cpu().numpy()
 
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(el_t.item())
+    elapsed_max = max_over_ranks(elapsed, dev)
     total_rti = world * B * args.steps
     value = total_rti / elapsed_max
 
