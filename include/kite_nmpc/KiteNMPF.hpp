@@ -121,6 +121,7 @@ public:
     // "return_status" of getStats() (kiteNMPF.cpp:303-313)
     std::string getStats() const {
         if (status_ & KITE_ST_NAN) return "Invalid_Number_Detected";
+        if (status_ & KITE_ST_STEP_REJECTED) return "Restoration_Failed";
         if (status_ & KITE_ST_QP_NOT_CONV) return "Maximum_Iterations_Exceeded";
         return "Solve_Succeeded";
     }

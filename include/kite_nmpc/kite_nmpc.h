@@ -54,6 +54,9 @@ extern "C" {
 #define KITE_ST_STATE_BOUND    8   /* predicted state outside lbx/ubx (states not
                                       enforced in the QP: everything but vx) */
 #define KITE_ST_THETA_WRAP    16   /* theta wrapped by 2*pi (kiteNMPF.cpp:212-221) */
+#define KITE_ST_STEP_REJECTED 32   /* QP residual >= 1e-6 or NaN: no step applied, the
+                                      shifted plan is kept (the reference applies the
+                                      failed iterate, kiteNMPF.cpp:303-313)          */
 
 /* ---- model parameters: kite_utils::LoadProperties (kite.cpp:7-76) ------
  * Field order == KiteProperties (kite.h:9-93) flattened.  52 doubles.     */

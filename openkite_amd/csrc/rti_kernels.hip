@@ -88,6 +88,9 @@ __device__ __forceinline__ double bcast_rowgroup(double v, int q) {
 struct OpAdd { __device__ double operator()(double a, double b) const { return a + b; } };
 struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
 struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
+// RTI step safeguard threshold on the final QP residual (oracle QP_STEP_ACCEPT)
+constexpr double QP_STEP_ACCEPT = 1e-6;
+
 // NaN-propagating max (fmax drops NaN: a poisoned KKT residual must never
 // read as converged)
 __device__ __forceinline__ double nmax(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
@@ -543,12 +546,15 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
                              double* vec, double* col) {
     const int N = C.N, n = C.n;
     // ---- expansion and trajectory update ------------------------------------
+    // step safeguard (oracle rti_one): a failed QP (residual >= 1e-6 or NaN)
+    // contributes no step; the shifted plan is kept and the gaps are closed
+    const bool accept = kkt < QP_STEP_ACCEPT;
     // physical step dw = D w_s into vec
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const int i = l + 64 * s;
-        if (i < n) vec[i] = w[s] * col_scale(C, i);
+        if (i < n) vec[i] = accept ? w[s] * col_scale(C, i) : 0.0;
     }
     __syncthreads();
     const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
@@ -633,6 +639,7 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         int32_t st = status[b];
         if (bad) st |= 1;
         if (!(kkt < 1e-8)) st |= 2;
+        if (!accept) st |= 32;
         if (bound && !bad) st |= 8;
         status[b] = st;
         if (kkt_out) kkt_out[b] = kkt;

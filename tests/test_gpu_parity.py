@@ -162,6 +162,46 @@ def test_rti_steps_vs_oracle(kp, cfgv):
     print(f"RTI GPU vs oracle worst relative error over 6 steps: {worst:.3e}")
 
 
+def test_long_closed_loop_vs_oracle(kp, cfgv):
+    """256 kites x 25 closed-loop steps along the oracle's trajectory: the
+    synthetic kites slow down onto the vx >= 2 bound, where a few QPs become
+    infeasible and the IPM diverges.  Every step starts the GPU from the
+    oracle's previous solution (set_solution), so each step is a parity check
+    from identical inputs; the step safeguard (status bit 32) must fire on the
+    same kite-steps, and the results must agree within RTI_TOL elsewhere."""
+    B, steps = 256, 25
+    x = x0_batch(B)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    diverged = np.zeros(B, bool)
+    rejected = 0
+    errs = []
+    try:
+        for step in range(steps):
+            if step > 0:
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0), nthreads=8)
+            assert not np.any(r["status"] & 1) and not np.any(st & 1)
+            same = (r["status"] & 32) == (st & 32)
+            diverged |= ~same
+            rejected += int(np.sum(st & 32))
+            # per kite, relative to max(1, |oracle|) of that kite's arrays
+            e = np.array([max(rel(r["traj"][k], Xo[k]), rel(r["ctrl"][k], Uo[k])) for k in range(B)])[same]
+            errs.append(e)
+            # near the bound some QPs are ill-posed (the oracle's own response to a
+            # 1e-15 perturbation of H reaches ~5e-7 there): statistical bar
+            assert np.mean(e < RTI_TOL) >= 0.99 and e.max() < 1e-4, (step, np.sort(e)[-3:])
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+    assert diverged.sum() <= 2, np.where(diverged)[0]
+    e = np.concatenate(errs)
+    print(f"long closed loop: {rejected} rejected QP steps in the oracle, {diverged.sum()} kites with differing "
+          f"safeguard decisions; kite-step errors median {np.median(e):.1e}, p99 {np.quantile(e, 0.99):.1e}, "
+          f"max {e.max():.1e}")
+
+
 def test_full_batch_properties():
     """BASELINE config 3 size (B = 4096, N = 20): size-independent properties."""
     B = 4096
