@@ -88,7 +88,7 @@ typedef struct kite_nmpc_config {
     int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
     int32_t qp_kernel;    /* 0: auto (MFMA-tiled QP when N == 20), 1: wave-scalar LDS QP,
                              2: MFMA-tiled (KITE_EINVAL unless N == 20) */
-    int32_t reserved;
+    int32_t delay_steps;  /* RK4 substeps of the delay-compensation prediction (4) */
     double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
     double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */
     double R[4];          /* control weights (kiteNMPF.cpp:33)                 */
@@ -102,6 +102,14 @@ typedef struct kite_nmpc_config {
     double path_q[4];     /* (w,x,y,z); P = vec(q^-1 (x) p (x) q)               */
     double theta_flex;    /* +- relaxation of theta, thetadot at t0 (kiteNMPF.cpp:226) */
     double min_speed;     /* caller-side vx clamp (nmpf_node.cpp:241-243); <= -INF disables */
+    double delay;         /* transport-delay compensation of the ROS node, fused into
+                             the step (nmpf_node.cpp:206-221): on warm steps the kite
+                             part of x0 is predicted over `delay` s under the previous
+                             u(t0) (RK4, delay_steps substeps; the node used CVODES)
+                             and theta, thetadot are taken from the previous trajectory
+                             at node round(delay/dt).  0 = off: KiteNMPF semantics, the
+                             caller passes the predicted state (default).  The node
+                             uses 0.1 (nmpf_node.cpp:74).                              */
 } kite_nmpc_config;
 
 /* ---- diagnostics: msg/mpc_diagnostic.msg (filled at nmpf_node.cpp:191-204) */

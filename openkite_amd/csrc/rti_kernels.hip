@@ -166,6 +166,17 @@ __global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, in
     double x0[NX];
     for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
     int32_t st = 0;
+    if (warm && C.delay > 0.0) {
+        // transport-delay compensation (nmpf_node.cpp:206-221): predict the
+        // measured kite state over `delay` under the previous u(t0); theta,
+        // thetadot from the previous trajectory at t0 + delay
+        const double up[NU] = {Ub[0], Ub[1], Ub[2], 0.0};
+        double xp[NX];
+        rk4_primal(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp);
+        for (int i = 0; i < 13; ++i) x0[i] = xp[i];
+        x0[13] = Xb[C.delay_node * NX + 13];
+        x0[14] = Xb[C.delay_node * NX + 14];
+    }
     const double twopi = 2.0 * M_PI;
     if (x0[13] > twopi) { x0[13] -= twopi; st |= 16; }
     else if (x0[13] < -twopi) { x0[13] += twopi; st |= 16; }

@@ -30,6 +30,8 @@ struct RtiConst {
     double lbx[15], ubx[15], lbu[4], ubu[4];
     double flex, min_speed;
     double path_R, path_alt, pq[4];
+    double delay;       // delay compensation [s] (0 = off)
+    int delay_steps, delay_node;
 };
 
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,

@@ -45,13 +45,14 @@ class NmpcConfig(ctypes.Structure):
     _fields_ = [
         ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("qp_iters", ctypes.c_int32), ("shift", ctypes.c_int32),
         ("device", ctypes.c_int32), ("timing", ctypes.c_int32), ("qp_kernel", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("delay_steps", ctypes.c_int32),
         ("dt", ctypes.c_double), ("Q", ctypes.c_double * 3), ("R", ctypes.c_double * 4), ("W", ctypes.c_double),
         ("Sx", ctypes.c_double * 15), ("Su", ctypes.c_double * 4),
         ("lbx", ctypes.c_double * 15), ("ubx", ctypes.c_double * 15),
         ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4),
         ("vref", ctypes.c_double), ("path_radius", ctypes.c_double), ("path_altitude", ctypes.c_double),
         ("path_q", ctypes.c_double * 4), ("theta_flex", ctypes.c_double), ("min_speed", ctypes.c_double),
+        ("delay", ctypes.c_double),
     ]
 
     def to_dict(self) -> dict:

@@ -68,15 +68,16 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
         path_R=2.65, path_alt=0.0,
         path_q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0],
         flex=0.78, min_speed=2.1,
+        delay=0.0, delay_steps=4,     # node transport delay 0.1 s (nmpf_node.cpp:74); 0 = KiteNMPF alone
     )
 
 
 def cfg_vector(c: Dict) -> np.ndarray:
     v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
          *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
-         c["flex"], c["min_speed"]]
+         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4)]
     a = np.array(v, dtype=np.float64)
-    assert a.size == 75
+    assert a.size == 77
     return a
 
 

@@ -162,6 +162,32 @@ def test_rti_steps_vs_oracle(kp, cfgv):
     print(f"RTI GPU vs oracle worst relative error over 6 steps: {worst:.3e}")
 
 
+def test_delay_compensation_vs_oracle(kp):
+    """Fused transport-delay compensation (config.delay = 0.1 s, the node's
+    default, nmpf_node.cpp:74): 5 closed-loop steps of 16 kites vs the oracle."""
+    B = 16
+    c = ffi.node_config()
+    c["delay"], c["delay_steps"] = 0.1, 4
+    cv = ffi.cfg_vector(c)
+    x = x0_batch(B, offset=4000)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(delay=0.1, delay_steps=4), B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    try:
+        for step in range(5):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            assert e < RTI_TOL, (step, e)
+            np.testing.assert_array_equal(r["status"], st)
+            # the plant: the measured state drifts from the prediction (so the
+            # compensation has work to do); theta/thetadot inputs are ignored when warm
+            x = Xo[:, 1, :].copy()
+            x[:, :3] *= 1.002
+            x[:, 13:] = 0.0
+    finally:
+        g.close()
+
+
 def test_long_closed_loop_vs_oracle(kp, cfgv):
     """256 kites x 25 closed-loop steps along the oracle's trajectory: the
     synthetic kites slow down onto the vx >= 2 bound, where a few QPs become

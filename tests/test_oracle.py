@@ -210,3 +210,28 @@ def test_qp_sensitivity_envelope(kp, cfgv):
         assert k0 < 1e-8 and k1 < 1e-8
         worst = max(worst, np.abs(w1 - w0).max() / max(1.0, np.abs(w0).max()))
     assert 1e-8 < worst < 1e-6, worst
+
+
+def test_delay_compensation_prologue(kp):
+    """Delay compensation (nmpf_node.cpp:206-221) in the oracle prologue: kite
+    state predicted over 0.1 s under the previous u(t0) with 4 RK4 substeps,
+    theta/thetadot from the previous trajectory at node round(0.1/0.05) = 2."""
+    N, M = 20, 2
+    c = ffi.node_config()
+    c["delay"], c["delay_steps"] = 0.1, 4
+    cv = ffi.cfg_vector(c)
+    x0 = np.zeros(15)
+    x0[:13] = ffi.synthetic_states(1, offset=5)[0]
+    st, X, U, _ = ffi.prologue(kp, cv, N, M, x0, np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+    X[:, 13] += 0.3
+    X[:, 14] += 1.7
+    U[0, :3] = [0.12, 0.01, -0.02]
+    st2, X2, U2, x0p = ffi.prologue(kp, cv, N, M, x0, X, U, warm=1)
+    up = np.array([0.12, 0.01, -0.02, 0.0])
+    pred = ffi.rk4(kp, x0, up, 0.025, 4)
+    np.testing.assert_array_equal(x0p[:13], pred[:13])
+    assert x0p[13] == X[2, 13] and x0p[14] == X[2, 14]
+    np.testing.assert_array_equal(X2[0], x0p)
+    # delay = 0: the measured state is used as given (KiteNMPF semantics)
+    st3, _, _, x0q = ffi.prologue(kp, ffi.cfg_vector(ffi.node_config()), N, M, x0, X, U, warm=1)
+    np.testing.assert_array_equal(x0q, x0)
