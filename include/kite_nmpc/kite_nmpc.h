@@ -57,6 +57,9 @@ extern "C" {
 #define KITE_ST_STEP_REJECTED 32   /* QP residual >= 1e-6 or NaN: no step applied, the
                                       shifted plan is kept (the reference applies the
                                       failed iterate, kiteNMPF.cpp:303-313)          */
+#define KITE_ST_RESTART       64   /* the warm start held non-finite values: this kite
+                                      was restarted cold, theta from the closest point
+                                      and thetadot = 0 (nmpf_node.cpp:225-236)        */
 
 /* ---- model parameters: kite_utils::LoadProperties (kite.cpp:7-76) ------
  * Field order == KiteProperties (kite.h:9-93) flattened.  52 doubles.     */

@@ -121,6 +121,29 @@ __device__ __forceinline__ void path_eval(const RtiConst& C, double th, double P
     dP[0] = dp.x; dP[1] = dp.y; dP[2] = dp.z;
 }
 
+// findClosestPointOnPath (kiteNMPF.cpp:358-391): <= 10 gradient steps of 1/4 on
+// 1/2 ||P(theta) - r|| (the non-squared norm as written, kiteNMPF.cpp:361)
+__device__ double closest_point_dev(const RtiConst& C, double px, double py, double pz, double guess) {
+    auto grad = [&](double th) {
+        double P[3], dP[3];
+        path_eval(C, th, P, dP);
+        const double e0 = P[0] - px, e1 = P[1] - py, e2 = P[2] - pz;
+        const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+        return 0.5 * (e0 * dP[0] + e1 * dP[1] + e2 * dP[2]) / nrm;
+    };
+    double th = guess;
+    double g = grad(th);
+    if (fabs(g) < 1e-2) { th = M_PI_2 + 0.1; g = grad(th); }
+    int counter = 0;
+    while (fabs(g) >= 1e-2) {
+        ++counter;
+        th -= 0.25 * g;
+        g = grad(th);
+        if (counter > 10) break;
+    }
+    return th;
+}
+
 // primal RK4 of the augmented 15-state model, M substeps of length h
 __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* u, double h, int M,
                            double* xo) {
@@ -166,6 +189,20 @@ __global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, in
     double x0[NX];
     for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
     int32_t st = 0;
+    if (warm) {
+        // a non-finite plan (a NaN iterate of a previous step) cannot seed a
+        // warm start: restart this kite cold, theta re-initialised by the
+        // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236)
+        bool finite = true;
+        for (int e = 0; e < (N + 1) * NX; ++e) finite &= isfinite(Xb[e]);
+        for (int e = 0; e < N * NU; ++e) finite &= isfinite(Ub[e]);
+        if (!finite) {
+            warm = 0;
+            st |= 64;
+            x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
+            x0[14] = 0.0;
+        }
+    }
     if (warm && C.delay > 0.0) {
         // transport-delay compensation (nmpf_node.cpp:206-221): predict the
         // measured kite state over `delay` under the previous u(t0); theta,
@@ -1123,25 +1160,8 @@ __global__ __launch_bounds__(64, 2) void k_closest_point(RtiConst C, int count, 
                                 const double* __restrict__ guess, double* __restrict__ theta) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
-    const double px = pos[(size_t)i * 3], py = pos[(size_t)i * 3 + 1], pz = pos[(size_t)i * 3 + 2];
-    auto grad = [&](double th) {
-        double P[3], dP[3];
-        path_eval(C, th, P, dP);
-        const double e0 = P[0] - px, e1 = P[1] - py, e2 = P[2] - pz;
-        const double nrm = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
-        return 0.5 * (e0 * dP[0] + e1 * dP[1] + e2 * dP[2]) / nrm;
-    };
-    double th = guess ? guess[i] : 0.0;
-    double g = grad(th);
-    if (fabs(g) < 1e-2) { th = M_PI_2 + 0.1; g = grad(th); }
-    int counter = 0;
-    while (fabs(g) >= 1e-2) {
-        ++counter;
-        th -= 0.25 * g;
-        g = grad(th);
-        if (counter > 10) break;
-    }
-    theta[i] = th;
+    theta[i] = closest_point_dev(C, pos[(size_t)i * 3], pos[(size_t)i * 3 + 1], pos[(size_t)i * 3 + 2],
+                                 guess ? guess[i] : 0.0);
 }
 
 // ---------------------------------------------------------------------------

@@ -23,6 +23,7 @@ DEFAULT_PARAMS = os.path.join(REPO, "data", "umx_radian.yaml")
 
 KITE_OK, KITE_EINVAL, KITE_EHIP, KITE_ENOMEM, KITE_ENODEV, KITE_EIO, KITE_EPARSE, KITE_ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
 ST_NAN, ST_QP_NOT_CONV, ST_MIN_SPEED, ST_STATE_BOUND, ST_THETA_WRAP, ST_STEP_REJECTED = 1, 2, 4, 8, 16, 32
+ST_RESTART = 64
 
 _PARAM_FIELDS = ["b", "c", "AR", "S", "lam", "St", "lt", "Sf", "lf", "Xac",
                  "mass", "Ixx", "Iyy", "Izz", "Ixz",

@@ -188,6 +188,32 @@ def test_delay_compensation_vs_oracle(kp):
         g.close()
 
 
+def test_restart_on_nonfinite_plan_vs_oracle(kp, cfgv):
+    """Kites whose warm start holds NaN restart cold (status bit 64) exactly as
+    in the oracle; the others continue warm."""
+    B = 16
+    x = x0_batch(B, offset=5000)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    try:
+        for step in range(3):
+            if step == 2:
+                Xo[3, 5, 1] = np.nan
+                Uo[9, 0, 0] = np.inf
+                x[3, 13] = np.nan
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            np.testing.assert_array_equal(r["status"], st)
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            assert e < RTI_TOL, (step, e)
+            x = Xo[:, 1, :].copy()
+        assert st[3] & 64 and st[9] & 64 and not np.any(np.delete(st, [3, 9]) & 64)
+        assert np.all(np.isfinite(r["traj"]))
+    finally:
+        g.close()
+
+
 def test_long_closed_loop_vs_oracle(kp, cfgv):
     """256 kites x 25 closed-loop steps along the oracle's trajectory: the
     synthetic kites slow down onto the vx >= 2 bound, where a few QPs become

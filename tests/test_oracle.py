@@ -235,3 +235,22 @@ def test_delay_compensation_prologue(kp):
     # delay = 0: the measured state is used as given (KiteNMPF semantics)
     st3, _, _, x0q = ffi.prologue(kp, ffi.cfg_vector(ffi.node_config()), N, M, x0, X, U, warm=1)
     np.testing.assert_array_equal(x0q, x0)
+
+
+def test_prologue_restarts_on_nonfinite_plan(kp, cfgv):
+    """A NaN in the warm start (a failed previous iterate) restarts the kite
+    cold: status bit 64, theta from the closest point, thetadot = 0."""
+    N, M = 20, 2
+    x0 = np.zeros(15)
+    x0[:13] = ffi.synthetic_states(1, offset=8)[0]
+    x0[13], x0[14] = np.nan, 3.0
+    X = np.zeros((N + 1, 15)); U = np.zeros((N, 4))
+    X[7, 2] = np.nan
+    st, Xw, Uw, x0w = ffi.prologue(kp, cfgv, N, M, x0, X, U, warm=1)
+    assert st & 64
+    th = ffi.closest_point(cfgv, x0[6:9], 0.0)
+    xc = x0.copy(); xc[13], xc[14] = th, 0.0
+    st2, Xc, Uc, _ = ffi.prologue(kp, cfgv, N, M, xc, np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+    np.testing.assert_array_equal(Xw, Xc)
+    np.testing.assert_array_equal(Uw, Uc)
+    assert st2 & 64 == 0
