@@ -203,6 +203,21 @@ int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
                        double* A, double* B);
 
 /* ---- introspection (tests, profiling) ---------------------------------- */
+/* ---- extended Kalman filter: KiteEKF (src/kite_estimation/kiteEKF.cpp) ---
+ * For each of `count` kites: propagate(dt) (kiteEKF.cpp:75-98: one RK4 step,
+ * A = I + J dt, P = A P A' + W) and, when z7 != NULL, the update of
+ * _estimate (kiteEKF.cpp:108-126) with H = [0_{7x6} I_7] (position r and
+ * quaternion q measured).  x13 (count x 13) and P169 (count x 13 x 13,
+ * row-major) are updated in place; u3 count x 3 (T, dE, dR); z7 count x 7;
+ * W169 / V49 shared by all kites.                                           */
+void kite_ekf_default_covariances(double* W169, double* V49, double* P0_169);  /* kiteEKF.cpp:6-13,26 */
+int kite_nmpc_ekf_step(kite_nmpc_ctx* ctx, int32_t count, double dt, double* x13, const double* u3,
+                       double* P169, const double* z7, const double* W169, const double* V49);
+/* Same on device pointers, asynchronous on the context stream.              */
+int kite_nmpc_ekf_step_device(kite_nmpc_ctx* ctx, int32_t count, double dt, double* d_x13,
+                              const double* d_u3, double* d_P169, const double* d_z7,
+                              const double* d_W169, const double* d_V49);
+
 /* Per-kernel device time [ms] of the last step (cfg.timing = 1):
  * [prologue, rk4_sens, condense, qp, total].  n = entries available (5).    */
 int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n);

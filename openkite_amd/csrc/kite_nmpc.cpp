@@ -565,6 +565,57 @@ int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15, cons
                      });
 }
 
+// ---- extended Kalman filter (kiteEKF.cpp) ----------------------------------
+void kite_ekf_default_covariances(double* W169, double* V49, double* P0_169) {
+    // kiteEKF.cpp:6-13: W = diag(S_v, S_w, S_r, S_q)^2, V = diag(...)^2; P0 = 10 W (:26)
+    const double sd_w[13] = {0.5, 0.5, 0.5, 0.5, 0.5, 0.5, 0.5, 0.1, 0.1, 0.01, 0.05, 0.05, 0.05};
+    const double sd_v[7] = {0.01, 0.01, 0.01, 0.0001, 0.005, 0.005, 0.005};
+    for (int i = 0; i < 169; ++i) {
+        if (W169) W169[i] = 0.0;
+        if (P0_169) P0_169[i] = 0.0;
+    }
+    for (int i = 0; i < 13; ++i) {
+        if (W169) W169[i * 13 + i] = sd_w[i] * sd_w[i];
+        if (P0_169) P0_169[i * 13 + i] = 10.0 * (sd_w[i] * sd_w[i]);
+    }
+    if (V49) {
+        for (int i = 0; i < 49; ++i) V49[i] = 0.0;
+        for (int i = 0; i < 7; ++i) V49[i * 7 + i] = sd_v[i] * sd_v[i];
+    }
+}
+
+int kite_nmpc_ekf_step_device(kite_nmpc_ctx* ctx, int32_t count, double dt, double* d_x13, const double* d_u3,
+                              double* d_P169, const double* d_z7, const double* d_W169, const double* d_V49) {
+    if (!ctx || count < 1 || !d_x13 || !d_u3 || !d_P169 || !d_W169 || (d_z7 && !d_V49) || !std::isfinite(dt))
+        return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(kite::launch_ekf(ctx->mc, count, dt, d_x13, d_u3, d_P169, d_z7, d_W169, d_V49, ctx->stream));
+    return KITE_OK;
+}
+
+int kite_nmpc_ekf_step(kite_nmpc_ctx* ctx, int32_t count, double dt, double* x13, const double* u3, double* P169,
+                       const double* z7, const double* W169, const double* V49) {
+    if (!ctx || count < 1 || !x13 || !u3 || !P169 || !W169 || (z7 && !V49) || !std::isfinite(dt)) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t c = count;
+    const size_t nx = c * 13, nu = c * 3, np = c * 169, nz = z7 ? c * 7 : 0;
+    int rc = ensure_scratch(ctx, (nx + nu + np + nz + 169 + 49) * sizeof(double));
+    if (rc) return rc;
+    double *dx = ctx->scratch, *du = dx + nx, *dP = du + nu, *dz = dP + np, *dW = dz + nz, *dV = dW + 169;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dx, x13, nx * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(du, u3, nu * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dP, P169, np * sizeof(double), hipMemcpyHostToDevice, s));
+    if (z7) HIP_TRY(hipMemcpyAsync(dz, z7, nz * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dW, W169, 169 * sizeof(double), hipMemcpyHostToDevice, s));
+    if (V49) HIP_TRY(hipMemcpyAsync(dV, V49, 49 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(kite::launch_ekf(ctx->mc, count, dt, dx, du, dP, z7 ? dz : nullptr, dW, dV, s));
+    HIP_TRY(hipMemcpyAsync(x13, dx, nx * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(P169, dP, np * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KITE_OK;
+}
+
 int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15, const double* u4, double tf,
                        int32_t M, double* xnext, double* A, double* Bm) {
     if (!ctx || count < 1 || !x15 || !u4 || !xnext || !A || !Bm || M < 1 || !std::isfinite(tf)) return KITE_EINVAL;

@@ -62,5 +62,8 @@ hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h
                                  const double* u, double* xo, double* A, double* Bm, hipStream_t s);
 hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,
                                 double* theta, hipStream_t s);
+// batched EKF propagate (+ update when z != nullptr), in place on x and Pc (ekf_kernels.hip)
+hipError_t launch_ekf(const ModelConst& P, int count, double dt, double* x, const double* u, double* Pc,
+                      const double* z, const double* W, const double* V, hipStream_t s);
 
 }  // namespace kite

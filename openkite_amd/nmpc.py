@@ -109,6 +109,12 @@ _SIGNATURES = {
     "kite_nmpc_timing_start": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
+    "kite_ekf_default_covariances": (None, [_DP, _DP, _DP]),
+    "kite_nmpc_ekf_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, _DP, _DP, _DP, _DP,
+                                          _DP, _DP]),
+    "kite_nmpc_ekf_step_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p]),
 }
 
 
@@ -308,6 +314,20 @@ class BatchNMPC:
         _check(lib().kite_nmpc_jacobian(self._h, x.shape[0], _p(x), _p(u), _p(Jx), _p(Ju)), "jacobian")
         return Jx, Ju
 
+    def ekf_step(self, x13, u3, P, dt: float, z7=None, W=None, V=None):
+        """Batched KiteEKF propagate (+ update when z7 is given); returns (x, P)."""
+        x = _f64(x13).reshape(-1, 13).copy()
+        c = x.shape[0]
+        Pm = _f64(P).reshape(c, 13, 13).copy()
+        u = _f64(u3).reshape(c, 3)
+        Wd, Vd, _ = ekf_default_covariances()
+        W = Wd if W is None else _f64(W).reshape(13, 13)
+        V = Vd if V is None else _f64(V).reshape(7, 7)
+        z = None if z7 is None else _f64(z7).reshape(c, 7)
+        _check(lib().kite_nmpc_ekf_step(self._h, c, float(dt), _p(x), _p(u), _p(Pm), _p(z), _p(W), _p(V)),
+               "ekf_step")
+        return x, Pm
+
     def predict(self, x15, u4, tf: float, steps: int = 1):
         x = _f64(x15).reshape(-1, 15); u = _f64(u4).reshape(-1, 4)
         xo = np.zeros_like(x)
@@ -336,6 +356,53 @@ class _ReturnStatus:
         if self.status & ST_QP_NOT_CONV:
             return "Maximum_Iterations_Exceeded"
         return "Solve_Succeeded"
+
+
+def ekf_default_covariances():
+    """(W, V, P0) of KiteEKF (kiteEKF.cpp:6-13, P0 = 10 W at :26)."""
+    W = np.zeros((13, 13)); V = np.zeros((7, 7)); P0 = np.zeros((13, 13))
+    lib().kite_ekf_default_covariances(_p(W), _p(V), _p(P0))
+    return W, V, P0
+
+
+class KiteEKF:
+    """Mirror of the reference ``KiteEKF`` (kiteEKF.h:10-55) for a batch of
+    kites on one GPU context: same setters/getters, ``propagate(dt)`` and
+    ``_estimate(measurement, dt)``; ``estimate(measurement, tstamp)`` takes
+    dt = tstamp - getTimeStamp() and, as in the reference (kiteEKF.cpp:100-105),
+    leaves the time stamp to ``setTime``."""
+
+    def __init__(self, batch: int = 1, params: Optional[KiteParams] = None, device: int = 0):
+        self._ctx = BatchNMPC(params if params is not None else load_properties(), default_config(device=device), batch)
+        self.batch = batch
+        self.W, self.V, P0 = ekf_default_covariances()
+        self.P = np.repeat(P0[None], batch, axis=0)
+        self.x = np.zeros((batch, 13))
+        self.u = np.zeros((batch, 3))
+        self.tstamp = 0.0
+
+    def close(self):
+        self._ctx.close()
+
+    def setProcessCovariance(self, W): self.W = _f64(W).reshape(13, 13).copy()
+    def setMeasurementCovariance(self, V): self.V = _f64(V).reshape(7, 7).copy()
+    def setEstimationCovariance(self, P): self.P = np.broadcast_to(_f64(P).reshape(-1, 13, 13), (self.batch, 13, 13)).copy()
+    def setEstimation(self, x): self.x = np.broadcast_to(_f64(x).reshape(-1, 13), (self.batch, 13)).copy()
+    def setControl(self, u): self.u = np.broadcast_to(_f64(u).reshape(-1, 3), (self.batch, 3)).copy()
+    def setTime(self, t): self.tstamp = float(t)
+    def getEstimation(self): return self.x.copy()
+    def getEstimationCovariance(self): return self.P.copy()
+    def getTimeStamp(self): return self.tstamp
+
+    def propagate(self, dt: float):
+        self.x, self.P = self._ctx.ekf_step(self.x, self.u, self.P, dt, None, self.W, self.V)
+
+    def _estimate(self, measurement, dt: float):
+        z = np.broadcast_to(_f64(measurement).reshape(-1, 7), (self.batch, 7))
+        self.x, self.P = self._ctx.ekf_step(self.x, self.u, self.P, dt, z, self.W, self.V)
+
+    def estimate(self, measurement, tstamp: float):
+        self._estimate(measurement, tstamp - self.tstamp)
 
 
 class KiteNMPF:

@@ -99,6 +99,7 @@ def lib():
             "orc_rhs_aug": (None, [dp, dp, dp, dp]),
             "orc_rhs_jac_cs": (None, [dp, dp, dp, dp]),
             "orc_rhs_jac_ad": (None, [dp, dp, dp, dp]),
+            "orc_ekf_step": (None, [dp, dp, dp, d, dp, dp, dp, dp]),
             "orc_rk4": (None, [dp, dp, dp, d, i, dp]),
             "orc_rk4_sens": (None, [dp, dp, dp, d, i, dp, dp, dp]),
             "orc_rk4_sens_cs": (None, [dp, dp, dp, d, i, dp, dp]),
@@ -144,6 +145,14 @@ def rhs_aug(kp, x15, u4):
     f = np.zeros(15)
     lib().orc_rhs_aug(_p(kp), _p(_f64(x15)), _p(_f64(u4)), _p(f))
     return f
+
+
+def ekf_step(kp, x13, u3, dt, P, z7, W, V):
+    """KiteEKF propagate (+ update when z7 is not None) for one kite; returns (x, P)."""
+    x = _f64(x13).copy(); Pm = _f64(P).reshape(13, 13).copy()
+    lib().orc_ekf_step(_p(kp), _p(x), _p(_f64(u3)), float(dt), _p(Pm), None if z7 is None else _p(_f64(z7)),
+                       _p(_f64(W)), _p(_f64(V)))
+    return x, Pm
 
 
 def rhs_jac(kp, x13, u3, method="ad"):

@@ -1,0 +1,95 @@
+"""Batched EKF (KiteEKF, src/kite_estimation/kiteEKF.cpp:75-126).
+
+CPU: the oracle restatement against its own definition (covariance symmetry,
+propagate = RK4 + A P A' + W with A from the golden-pinned Jacobian, update
+reduces the measured-state covariance).  GPU: the HIP kernel against the
+oracle on the same inputs, propagate-only and propagate + update."""
+import numpy as np
+import pytest
+
+import openkite_amd as ok
+from oracle import ffi
+
+
+def _inputs(B, seed=3):
+    rng = np.random.default_rng(seed)
+    x = ffi.synthetic_states(B, offset=600)
+    u = np.column_stack([rng.uniform(0.1, 0.15, B), rng.uniform(-0.1, 0.1, (B, 2))])
+    W, V, P0 = ok.ekf_default_covariances()
+    P = np.repeat(P0[None], B, axis=0)
+    G = rng.normal(size=(B, 13, 13)) * 0.01
+    P = P + G @ G.transpose(0, 2, 1)                      # a generic SPD covariance
+    z = x[:, 6:13] + rng.normal(size=(B, 7)) * 0.01
+    return x, u, P, z, W, V
+
+
+def test_default_covariances_match_reference():
+    W, V, P0 = ok.ekf_default_covariances()
+    sw = np.array([0.5] * 7 + [0.1, 0.1, 0.01, 0.05, 0.05, 0.05])   # diagcat(S_V, S_W, S_R, S_Q)
+    np.testing.assert_array_equal(np.diag(W), sw ** 2)
+    np.testing.assert_array_equal(np.diag(V), np.array([0.01, 0.01, 0.01, 0.0001, 0.005, 0.005, 0.005]) ** 2)
+    np.testing.assert_array_equal(P0, 10 * W)
+    assert np.count_nonzero(W - np.diag(np.diag(W))) == 0
+
+
+def test_oracle_ekf_propagate_and_update(kp):
+    x, u, P, z, W, V = _inputs(4)
+    dt = 0.02
+    for b in range(4):
+        xp, Pp = ffi.ekf_step(kp, x[b], u[b], dt, P[b], None, W, V)
+        J = ffi.rhs_jac(kp, x[b], u[b])[:, :13]
+        A = np.eye(13) + J * dt
+        np.testing.assert_allclose(Pp, A @ P[b] @ A.T + W, rtol=1e-13, atol=1e-15)
+        x15 = np.zeros(15); x15[:13] = x[b]
+        np.testing.assert_array_equal(xp, ffi.rk4(kp, x15, np.r_[u[b], 0.0], dt, 1)[:13])
+        xu, Pu = ffi.ekf_step(kp, x[b], u[b], dt, P[b], z[b], W, V)
+        H = np.hstack([np.zeros((7, 6)), np.eye(7)])
+        S = H @ Pp @ H.T + V
+        K = Pp @ H.T @ np.linalg.inv(S)
+        np.testing.assert_allclose(xu, xp + K @ (z[b] - H @ xp), rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(Pu, (np.eye(13) - K @ H) @ Pp, rtol=1e-10, atol=1e-14)
+        assert np.trace(Pu[6:, 6:]) < np.trace(Pp[6:, 6:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("update", [False, True])
+def test_gpu_ekf_vs_oracle(kp, update):
+    B = 4096
+    x, u, P, z, W, V = _inputs(B)
+    dt = 0.02
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), 1)
+    try:
+        xg, Pg = g.ekf_step(x, u, P, dt, z if update else None, W, V)
+    finally:
+        g.close()
+    for b in range(0, B, 97):
+        xo, Po = ffi.ekf_step(kp, x[b], u[b], dt, P[b], z[b] if update else None, W, V)
+        np.testing.assert_allclose(xg[b], xo, rtol=1e-12, atol=1e-13)
+        np.testing.assert_allclose(Pg[b], Po, rtol=1e-11, atol=1e-13)
+    assert np.all(np.isfinite(xg)) and np.all(np.isfinite(Pg))
+
+
+@pytest.mark.gpu
+def test_kite_ekf_mirror_tracks_plant():
+    """KiteEKF mirror on a noisy simulated kite: the estimate error shrinks."""
+    B = 64
+    rng = np.random.default_rng(11)
+    truth = ffi.synthetic_states(B, offset=700)
+    ekf = ok.KiteEKF(B)
+    try:
+        est = truth.copy()
+        est[:, :6] += rng.normal(size=(B, 6)) * 0.3          # wrong velocities / rates
+        ekf.setEstimation(est)
+        u = np.tile([0.12, 0.0, 0.0], (B, 1))
+        ekf.setControl(u)
+        err0 = np.abs(ekf.getEstimation() - truth)[:, :3].mean()
+        for _ in range(25):
+            x15 = np.zeros((B, 15)); x15[:, :13] = truth
+            truth = ekf._ctx.predict(x15, np.column_stack([u, np.zeros(B)]), 0.02, 1)[:, :13]
+            z = truth[:, 6:13] + rng.normal(size=(B, 7)) * np.array([0.01] * 3 + [1e-4, 5e-3, 5e-3, 5e-3])
+            ekf._estimate(z, 0.02)
+        err1 = np.abs(ekf.getEstimation() - truth)[:, :3].mean()
+        assert np.all(np.isfinite(ekf.getEstimationCovariance()))
+        assert err1 < 0.5 * err0, (err0, err1)
+    finally:
+        ekf.close()
