@@ -203,6 +203,35 @@ int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
                        double* A, double* B);
 
 /* ---- introspection (tests, profiling) ---------------------------------- */
+/* ---- reference formulation: Chebyshev collocation (chebyshev.hpp) -------
+ * Evaluates the reference's own NLP functions for `count` points
+ * z = [X (nodes x 15) | U (nodes x 4)], nodes = poly_order*num_segments + 1,
+ * in the reference's (optionally scaled) variables:
+ *   G = (CompDiff (x) I15) X - t_scale * SODE(X_i, U_i)      (chebyshev.hpp:241-271)
+ *   J = mayer_scale * M(X_0) + sum_seg t_scale sum_m w_m L(X, U) (:280-333)
+ * with t_scale = (tf - t0) / (2 num_segments), SODE(x, u) = Sx f_aug(x/Sx, u/Su)
+ * (kiteNMPF.cpp:100-104), L = Q.res^2 + W (vref - x14)^2 [+ R.u^2],
+ * res = Sx_r P(x13 / Sx13) - x(6:9), M = Q.res^2 (kiteNMPF.cpp:117-143).
+ * jac (nullable): per node the 15 x 19 block d SODE / d [x, u] at (X_i, U_i);
+ * the constraint Jacobian is dG/dX = CompDiff (x) I - t_scale blockdiag(jac_x),
+ * dG/dU = -t_scale blockdiag(jac_u).                                         */
+typedef struct kite_colloc_config {
+    int32_t poly_order;     /* 5 (kiteNMPF.cpp:83); 10 in full_generics_test     */
+    int32_t num_segments;   /* 2 (kiteNMPF.cpp:82); 1 in full_generics_test      */
+    int32_t use_R;          /* 1: L includes R u^2 (NMPF); 0: full_generics_test */
+    int32_t reserved;
+    double t0, tf;
+    double Q[3], R[4], W;
+    double vref;            /* in the formulation's variables (Sx14 * v when scaled) */
+    double mayer_scale;     /* 1 (NMPF), 2 (full_generics_test)                   */
+    double Sx[15], Su[4];   /* 1 = unscaled                                       */
+    double path_radius, path_altitude, path_q[4];
+} kite_colloc_config;
+/* The NMPF's setup (kiteNMPF.cpp:80-143 with the node's scaling and path).  */
+void kite_colloc_default_config(kite_colloc_config* cfg);
+int kite_nmpc_colloc_eval(kite_nmpc_ctx* ctx, const kite_colloc_config* cfg, int32_t count, const double* z,
+                          double* G, double* J, double* jac);
+
 /* ---- extended Kalman filter: KiteEKF (src/kite_estimation/kiteEKF.cpp) ---
  * For each of `count` kites: propagate(dt) (kiteEKF.cpp:75-98: one RK4 step,
  * A = I + J dt, P = A P A' + W) and, when z7 != NULL, the update of

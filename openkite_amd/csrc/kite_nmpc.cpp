@@ -565,6 +565,114 @@ int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15, cons
                      });
 }
 
+// ---- Chebyshev collocation evaluator (chebyshev.hpp) ------------------------
+extern "C++" {
+namespace {
+// CGL differentiation matrix of degree n on x_j = cos(j pi / n) (chebyshev.hpp:130-153)
+std::vector<double> cheb_D(int n) {
+    const int m = n + 1;
+    std::vector<double> x(m), c(m), D((size_t)m * m);
+    for (int j = 0; j < m; ++j) {
+        x[j] = std::cos(j * (M_PI / n));
+        c[j] = ((j == 0 || j == n) ? 2.0 : 1.0) * ((j % 2) ? -1.0 : 1.0);
+    }
+    for (int i = 0; i < m; ++i) {       // Dn = c (1/c)' / (dX + I);  D = Dn - diag(rowsum(Dn))
+        double row = 0.0;
+        for (int j = 0; j < m; ++j) {
+            const double v = (c[i] / c[j]) / (x[i] - x[j] + (i == j ? 1.0 : 0.0));
+            D[(size_t)i * m + j] = v;
+            row += v;
+        }
+        D[(size_t)i * m + i] -= row;
+    }
+    return D;
+}
+// Clenshaw-Curtis weights on the CGL points (chebyshev.hpp:156-195)
+std::vector<double> cheb_weights(int n) {
+    std::vector<double> w(n + 1, 0.0), v(std::max(0, n - 1), 1.0);
+    auto th = [&](int j) { return j * (M_PI / n); };
+    if (n % 2 == 0) {
+        w[0] = w[n] = 1.0 / ((double)n * n - 1.0);
+        for (int k = 1; k <= n / 2 - 1; ++k)
+            for (int i = 0; i < n - 1; ++i) v[i] -= 2.0 * std::cos(2.0 * k * th(i + 1)) / (4.0 * k * k - 1.0);
+        for (int i = 0; i < n - 1; ++i) v[i] -= std::cos(n * th(i + 1)) / ((double)n * n - 1.0);
+    } else {
+        w[0] = w[n] = 1.0 / ((double)n * n);
+        for (int k = 1; k <= (n - 1) / 2; ++k)
+            for (int i = 0; i < n - 1; ++i) v[i] -= 2.0 * std::cos(2.0 * k * th(i + 1)) / (4.0 * k * k - 1.0);
+    }
+    for (int i = 0; i < n - 1; ++i) w[i + 1] = 2.0 * v[i] / n;
+    return w;
+}
+}  // namespace
+}  // extern "C++"
+
+void kite_colloc_default_config(kite_colloc_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    kite_nmpc_config n;
+    kite_nmpc_default_config(&n);
+    c->poly_order = 5; c->num_segments = 2; c->use_R = 1;       // kiteNMPF.cpp:82-83
+    c->t0 = 0.0; c->tf = 1.0;                                    // kiteNMPF.cpp:88
+    for (int i = 0; i < 3; ++i) c->Q[i] = n.Q[i];
+    for (int i = 0; i < 4; ++i) { c->R[i] = n.R[i]; c->Su[i] = n.Su[i]; }
+    c->W = n.W;
+    for (int i = 0; i < 15; ++i) c->Sx[i] = n.Sx[i];
+    c->vref = n.Sx[14] * n.vref;                                 // setReferenceVelocity (kiteNMPF.h:34)
+    c->mayer_scale = 1.0;
+    c->path_radius = n.path_radius; c->path_altitude = n.path_altitude;
+    for (int i = 0; i < 4; ++i) c->path_q[i] = n.path_q[i];
+}
+
+int kite_nmpc_colloc_eval(kite_nmpc_ctx* ctx, const kite_colloc_config* cfg, int32_t count, const double* z,
+                          double* G, double* J, double* jac) {
+    if (!ctx || !cfg || count < 1 || !z || !G || !J) return KITE_EINVAL;
+    const int P = cfg->poly_order, S = cfg->num_segments, n = P * S + 1;
+    if (P < 1 || S < 1 || n > 32 || !(cfg->tf > cfg->t0)) return KITE_EINVAL;
+    for (int i = 0; i < 15; ++i) if (!(cfg->Sx[i] != 0.0) || !std::isfinite(cfg->Sx[i])) return KITE_EINVAL;
+    for (int i = 0; i < 4; ++i) if (!(cfg->Su[i] != 0.0) || !std::isfinite(cfg->Su[i])) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    // composite differentiation matrix (chebyshev.hpp:198-232) and node weights
+    const std::vector<double> D = cheb_D(P), w = cheb_weights(P);
+    std::vector<double> tab((size_t)n * n + n, 0.0);
+    if (S < 2) {
+        for (int i = 0; i <= P; ++i) for (int j = 0; j <= P; ++j) tab[(size_t)i * n + j] = D[(size_t)i * (P + 1) + j];
+    } else {
+        for (int i = 0; i <= P; ++i)
+            for (int j = 0; j <= P; ++j) tab[(size_t)(n - P - 1 + i) * n + (n - P - 1 + j)] = D[(size_t)i * (P + 1) + j];
+        for (int k = 0; k < (S - 1) * P; k += P)
+            for (int i = 0; i < P; ++i)
+                for (int j = 0; j <= P; ++j) tab[(size_t)(k + i) * n + (k + j)] = D[(size_t)i * (P + 1) + j];
+    }
+    kite::CollocConst C;
+    std::memset(&C, 0, sizeof(C));
+    C.nodes = n; C.use_R = cfg->use_R;
+    C.t_scale = (cfg->tf - cfg->t0) / (2.0 * S);
+    C.mayer_scale = cfg->mayer_scale;
+    for (int k = 0; k < S; ++k)                                  // chebyshev.hpp:303-322
+        for (int m = 0; m <= P; ++m) tab[(size_t)n * n + k * P + m] += C.t_scale * w[m];
+    for (int i = 0; i < 3; ++i) C.Q[i] = cfg->Q[i];
+    for (int i = 0; i < 4; ++i) { C.R[i] = cfg->R[i]; C.Su[i] = cfg->Su[i]; C.iSu[i] = 1.0 / cfg->Su[i]; }
+    for (int i = 0; i < 15; ++i) { C.Sx[i] = cfg->Sx[i]; C.iSx[i] = 1.0 / cfg->Sx[i]; }
+    C.W = cfg->W; C.vref = cfg->vref;
+    C.path_R = cfg->path_radius; C.path_alt = cfg->path_altitude;
+    for (int i = 0; i < 4; ++i) C.pq[i] = cfg->path_q[i];
+
+    const size_t c = count, nz = (size_t)n * 19, ng = (size_t)n * 15, nj = jac ? c * n * 15 * 19 : 0;
+    int rc = ensure_scratch(ctx, (tab.size() + c * nz + c * ng + c + nj) * sizeof(double));
+    if (rc) return rc;
+    double *dtab = ctx->scratch, *dz = dtab + tab.size(), *dG = dz + c * nz, *dJ = dG + c * ng, *djac = dJ + c;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dtab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(dz, z, c * nz * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(kite::launch_colloc(ctx->mc, C, count, dtab, dz, dG, dJ, jac ? djac : nullptr, s));
+    HIP_TRY(hipMemcpyAsync(G, dG, c * ng * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(J, dJ, c * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (jac) HIP_TRY(hipMemcpyAsync(jac, djac, nj * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return KITE_OK;
+}
+
 // ---- extended Kalman filter (kiteEKF.cpp) ----------------------------------
 void kite_ekf_default_covariances(double* W169, double* V49, double* P0_169) {
     // kiteEKF.cpp:6-13: W = diag(S_v, S_w, S_r, S_q)^2, V = diag(...)^2; P0 = 10 W (:26)

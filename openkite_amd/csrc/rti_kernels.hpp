@@ -62,6 +62,17 @@ hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h
                                  const double* u, double* xo, double* A, double* Bm, hipStream_t s);
 hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,
                                 double* theta, hipStream_t s);
+// Chebyshev collocation evaluator (colloc_kernels.hip): constants of one formulation
+struct CollocConst {
+    int nodes, use_R;
+    double t_scale, mayer_scale;
+    double Q[3], R[4], W, vref;
+    double Sx[15], Su[4], iSx[15], iSu[4];
+    double path_R, path_alt, pq[4];
+};
+// tab = CompDiff (nodes x nodes, row-major) followed by the node weights (nodes)
+hipError_t launch_colloc(const ModelConst& P, const CollocConst& C, int count, const double* tab, const double* z,
+                         double* G, double* J, double* jac, hipStream_t s);
 // batched EKF propagate (+ update when z != nullptr), in place on x and Pc (ekf_kernels.hip)
 hipError_t launch_ekf(const ModelConst& P, int count, double dt, double* x, const double* u, double* Pc,
                       const double* z, const double* W, const double* V, hipStream_t s);

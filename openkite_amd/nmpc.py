@@ -64,6 +64,25 @@ class NmpcConfig(ctypes.Structure):
         return d
 
 
+class CollocConfig(ctypes.Structure):
+    """kite_colloc_config: the reference's collocation NLP functions (chebyshev.hpp)."""
+    _fields_ = [
+        ("poly_order", ctypes.c_int32), ("num_segments", ctypes.c_int32), ("use_R", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("t0", ctypes.c_double), ("tf", ctypes.c_double), ("Q", ctypes.c_double * 3), ("R", ctypes.c_double * 4),
+        ("W", ctypes.c_double), ("vref", ctypes.c_double), ("mayer_scale", ctypes.c_double),
+        ("Sx", ctypes.c_double * 15), ("Su", ctypes.c_double * 4),
+        ("path_radius", ctypes.c_double), ("path_altitude", ctypes.c_double), ("path_q", ctypes.c_double * 4),
+    ]
+
+    def to_dict(self) -> dict:
+        d = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            d[name] = list(v) if hasattr(v, "__len__") else v
+        return d
+
+
 class MpcDiagnostic(ctypes.Structure):
     """msg/mpc_diagnostic.msg field order."""
     _fields_ = [("pos_error", ctypes.c_double), ("vel_error", ctypes.c_double), ("cost", ctypes.c_double),
@@ -110,6 +129,8 @@ _SIGNATURES = {
     "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
     "kite_ekf_default_covariances": (None, [_DP, _DP, _DP]),
+    "kite_colloc_default_config": (None, [ctypes.c_void_p]),
+    "kite_nmpc_colloc_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP]),
     "kite_nmpc_ekf_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, _DP, _DP, _DP, _DP,
                                           _DP, _DP]),
     "kite_nmpc_ekf_step_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_double, ctypes.c_void_p,
@@ -314,6 +335,17 @@ class BatchNMPC:
         _check(lib().kite_nmpc_jacobian(self._h, x.shape[0], _p(x), _p(u), _p(Jx), _p(Ju)), "jacobian")
         return Jx, Ju
 
+    def colloc_eval(self, cfg: "CollocConfig", z, jac: bool = False):
+        """Reference collocation residual G (count x n*15), cost J (count) and,
+        with jac, the per-node blocks d SODE / d [x, u] (count x n x 15 x 19)."""
+        n = cfg.poly_order * cfg.num_segments + 1
+        zz = _f64(z).reshape(-1, n * 19)
+        c = zz.shape[0]
+        G = np.zeros((c, n * 15)); J = np.zeros(c)
+        Jb = np.zeros((c, n, 15, 19)) if jac else None
+        _check(lib().kite_nmpc_colloc_eval(self._h, ctypes.byref(cfg), c, _p(zz), _p(G), _p(J), _p(Jb)), "colloc_eval")
+        return (G, J, Jb) if jac else (G, J)
+
     def ekf_step(self, x13, u3, P, dt: float, z7=None, W=None, V=None):
         """Batched KiteEKF propagate (+ update when z7 is given); returns (x, P)."""
         x = _f64(x13).reshape(-1, 13).copy()
@@ -356,6 +388,20 @@ class _ReturnStatus:
         if self.status & ST_QP_NOT_CONV:
             return "Maximum_Iterations_Exceeded"
         return "Solve_Succeeded"
+
+
+def colloc_default_config(**overrides) -> CollocConfig:
+    """The NMPF's collocation setup (kiteNMPF.cpp:80-143 + node scaling/path)."""
+    c = CollocConfig()
+    lib().kite_colloc_default_config(ctypes.byref(c))
+    for k, v in overrides.items():
+        cur = getattr(c, k)
+        if hasattr(cur, "__len__"):
+            for i, vi in enumerate(v):
+                cur[i] = vi
+        else:
+            setattr(c, k, v)
+    return c
 
 
 def ekf_default_covariances():

@@ -100,6 +100,7 @@ def lib():
             "orc_rhs_jac_cs": (None, [dp, dp, dp, dp]),
             "orc_rhs_jac_ad": (None, [dp, dp, dp, dp]),
             "orc_ekf_step": (None, [dp, dp, dp, d, dp, dp, dp, dp]),
+            "orc_colloc_eval": (None, [dp, dp, i, dp, dp, dp, dp]),
             "orc_rk4": (None, [dp, dp, dp, d, i, dp]),
             "orc_rk4_sens": (None, [dp, dp, dp, d, i, dp, dp, dp]),
             "orc_rk4_sens_cs": (None, [dp, dp, dp, d, i, dp, dp]),
@@ -145,6 +146,30 @@ def rhs_aug(kp, x15, u4):
     f = np.zeros(15)
     lib().orc_rhs_aug(_p(kp), _p(_f64(x15)), _p(_f64(u4)), _p(f))
     return f
+
+
+COLLOC_KEYS = ["poly_order", "num_segments", "use_R", "t0", "tf", "Q", "R", "W", "vref", "mayer_scale", "Sx", "Su",
+               "path_radius", "path_altitude", "path_q"]
+
+
+def colloc_vector(c: Dict) -> np.ndarray:
+    v = []
+    for k in COLLOC_KEYS:
+        x = c[k]
+        v.extend(x if isinstance(x, (list, tuple, np.ndarray)) else [x])
+    a = np.array(v, dtype=np.float64)
+    assert a.size == 40
+    return a
+
+
+def colloc_eval(kp, c: Dict, z, jac=False):
+    """Reference collocation G, J (and Jacobian blocks) at points z (count x nz)."""
+    z = _f64(z).reshape(-1, (c["poly_order"] * c["num_segments"] + 1) * 19)
+    cnt, n = z.shape[0], c["poly_order"] * c["num_segments"] + 1
+    G = np.zeros((cnt, n * 15)); J = np.zeros(cnt)
+    Jb = np.zeros((cnt, n, 15, 19)) if jac else None
+    lib().orc_colloc_eval(_p(kp), _p(colloc_vector(c)), cnt, _p(z), _p(G), _p(J), None if Jb is None else _p(Jb))
+    return (G, J, Jb) if jac else (G, J)
 
 
 def ekf_step(kp, x13, u3, dt, P, z7, W, V):
