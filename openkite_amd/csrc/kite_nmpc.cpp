@@ -499,6 +499,15 @@ int kite_nmpc_set_solution(kite_nmpc_ctx* ctx, const double* traj, const double*
     const size_t B = ctx->B, N = ctx->cfg.N;
     HIP_TRY(hipMemcpyAsync(ctx->X, traj, B * (N + 1) * 15 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->U, ctrl, B * N * 4 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    // non-finite plans are flagged like a NaN iterate: the next step restarts them cold
+    std::vector<int32_t> st(B, 0);
+    for (size_t b = 0; b < B; ++b) {
+        bool fin = true;
+        for (size_t e = 0; e < (N + 1) * 15; ++e) fin &= std::isfinite(traj[b * (N + 1) * 15 + e]);
+        for (size_t e = 0; e < N * 4; ++e) fin &= std::isfinite(ctrl[b * N * 4 + e]);
+        st[b] = fin ? 0 : KITE_ST_NAN;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->status, st.data(), B * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->warm = true;
     return KITE_OK;

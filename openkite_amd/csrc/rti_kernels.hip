@@ -17,6 +17,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "kite_model.hpp"
 #include "rti_kernels.hpp"
 
@@ -192,11 +194,10 @@ __global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, in
     if (warm) {
         // a non-finite plan (a NaN iterate of a previous step) cannot seed a
         // warm start: restart this kite cold, theta re-initialised by the
-        // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236)
-        bool finite = true;
-        for (int e = 0; e < (N + 1) * NX; ++e) finite &= isfinite(Xb[e]);
-        for (int e = 0; e < N * NU; ++e) finite &= isfinite(Ub[e]);
-        if (!finite) {
+        // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236).
+        // The previous epilogue flagged it (KITE_ST_NAN: non-finite X or U);
+        // kite_nmpc_set_solution flags injected plans the same way.
+        if (status[b] & 1) {
             warm = 0;
             st |= 64;
             x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
@@ -329,9 +330,6 @@ __global__ __launch_bounds__(RK_T, 2) void k_rk4_sens(ModelConst P, int B, int N
 // MFMA accumulators) with v_mfma_f64_16x16x4_f64.  Column n of W_ext is the
 // residual value, so H_ext[n][:] is the gradient.
 // ---------------------------------------------------------------------------
-constexpr int NP = 96;          // padded QP dimension (6 tiles of 16)
-constexpr int WLD = 112;        // LDS row stride of the W chunk (doubles): 2*WLD % 64 == 32
-constexpr int NTILE = 21;       // lower-triangular 16x16 tiles of 96x96
 constexpr int QP_NTA = 5;       // tiled QP: control block 4N = 80 = 5 tiles (N = 20)
 constexpr int QP_NTILE = QP_NTA * (QP_NTA + 1) / 2;   // 15 lower tiles
 
@@ -350,6 +348,26 @@ __device__ __forceinline__ double col_rdiag(const RtiConst& C, int j) {
     if (j < 4 * N) return C.Rdiag[3];
     return 0.0;
 }
+// the per-column scaling constants in registers (select-indexed: no dynamic
+// indexing into the kernel-argument struct, which would copy it to scratch)
+struct ColConst {
+    int N;
+    double iSu0, iSu1, iSu2, iSu3, iSx13, iSx14, Rd0, Rd1, Rd2, Rd3;
+};
+__device__ __forceinline__ ColConst col_const(const RtiConst& C) {
+    return ColConst{C.N, 1.0 / C.Su[0], 1.0 / C.Su[1], 1.0 / C.Su[2], 1.0 / C.Su[3], 1.0 / C.Sx13, 1.0 / C.Sx14,
+                    C.Rdiag[0], C.Rdiag[1], C.Rdiag[2], C.Rdiag[3]};
+}
+__device__ __forceinline__ double col_scale(const ColConst& K, int j) {
+    if (j < 3 * K.N) { const int c = j % 3; return c == 0 ? K.iSu0 : (c == 1 ? K.iSu1 : K.iSu2); }
+    if (j < 4 * K.N) return K.iSu3;
+    return j == 4 * K.N ? K.iSx13 : K.iSx14;
+}
+__device__ __forceinline__ double col_rdiag(const ColConst& K, int j) {
+    if (j < 3 * K.N) { const int c = j % 3; return c == 0 ? K.Rd0 : (c == 1 ? K.Rd1 : K.Rd2); }
+    if (j < 4 * K.N) return K.Rd3;
+    return 0.0;
+}
 __device__ __forceinline__ double col_ubar(const RtiConst& C, const double* Ub, int j) {
     const int N = C.N;
     if (j < 3 * N) return Ub[(j / 3) * NU + (j % 3)];
@@ -357,44 +375,114 @@ __device__ __forceinline__ double col_ubar(const RtiConst& C, const double* Ub, 
     return 0.0;
 }
 
-__global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double* __restrict__ X,
-                                                 const double* __restrict__ U,
-                                                 const double* __restrict__ AB,
-                                                 const double* __restrict__ DEF,
-                                                 double* __restrict__ Hs, double* __restrict__ hs,
-                                                 double* __restrict__ Cr, double* __restrict__ cl,
-                                                 double* __restrict__ cu, double* __restrict__ hmax, int tiled,
-                                                 double* __restrict__ Htl, double* __restrict__ Hab,
-                                                 double* __restrict__ Hbb) {
+// Condensing kernel, NW = 1..4 wavefronts per instance (CondenseGeom).
+//   threads t < 3N : column t of G (kite control (k=t/3, c=t%3)), 13 rows in VGPRs
+//   thread  3N     : affine column g (propagated defects)
+//   wave w         : MFMA accumulators of the lower tiles in its tile-row range
+//                    of H_ext (NR = ceil((n+1)/16) rows, balanced tile counts)
+// The affine column's values are shared through LDS (sG), the 16-row W chunk
+// (4 nodes) through LDS; every wave folds each chunk into its own tiles.
+template <int NR>
+struct CondenseGeom {
+    static constexpr int T = NR * (NR + 1) / 2;                        // lower tiles of H_ext
+    static constexpr int NW = T <= 10 ? 1 : ((T + 11) / 12 > 4 ? 4 : (T + 11) / 12);   // waves per instance
+    // first tile row of wave w: the row boundary whose tile count is closest
+    // to w T / NW (balances the accumulators of the waves)
+    static constexpr int lo(int w) {
+        if (w <= 0) return 0;
+        if (w >= NW) return NR;
+        int best = 0;
+        for (int r = 1; r < NR; ++r) {
+            const int d0 = 2 * NW * (r * (r + 1) / 2) - 2 * w * T;
+            const int d1 = 2 * NW * (best * (best + 1) / 2) - 2 * w * T;
+            if ((d0 < 0 ? -d0 : d0) < (d1 < 0 ? -d1 : d1)) best = r;
+        }
+        return best < lo(w - 1) ? lo(w - 1) : best;
+    }
+    static constexpr int tiles(int w) { return (lo(w + 1) * (lo(w + 1) + 1) - lo(w) * (lo(w) + 1)) / 2; }
+    static constexpr int acc() {
+        int m = 1;
+        for (int w = 0; w < NW; ++w) m = tiles(w) > m ? tiles(w) : m;
+        return m;
+    }
+    static constexpr int ACC = acc();
+    static constexpr int WLD = 16 * NR + ((NR % 2 == 0) ? 16 : 32);   // 2*WLD % 64 == 32: conflict-free
+};
+
+// Per-wave tile loops with compile-time tile coordinates: wave W owns the
+// lower tiles (I, J <= I) of tile rows [lo(W), lo(W+1)), accumulator slot Q.
+template <int NR, int W, int I, int J, int Q>
+__device__ __forceinline__ void fold_rec(double4v* acc, const double* fr) {
+    if constexpr (I < CondenseGeom<NR>::lo(W + 1)) {
+        acc[Q] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[I], fr[J], acc[Q], 0, 0, 0);
+        if constexpr (J < I) fold_rec<NR, W, I, J + 1, Q + 1>(acc, fr);
+        else fold_rec<NR, W, I + 1, 0, Q + 1>(acc, fr);
+    }
+}
+template <int NR, int W>
+__device__ __forceinline__ void wave_fold(int w, double4v* acc, const double* fr) {
+    if (w == W) fold_rec<NR, W, CondenseGeom<NR>::lo(W), 0, 0>(acc, fr);
+    else if constexpr (W + 1 < CondenseGeom<NR>::NW) wave_fold<NR, W + 1>(w, acc, fr);
+}
+template <int NR, int W, int I, int J, int Q, class F>
+__device__ __forceinline__ void put_rec(const double4v* acc, F& put) {
+    if constexpr (I < CondenseGeom<NR>::lo(W + 1)) {
+        put(I, J, acc[Q]);
+        if constexpr (J < I) put_rec<NR, W, I, J + 1, Q + 1>(acc, put);
+        else put_rec<NR, W, I + 1, 0, Q + 1>(acc, put);
+    }
+}
+template <int NR, int W, class F>
+__device__ __forceinline__ void wave_put(int w, const double4v* acc, F& put) {
+    if (w == W) put_rec<NR, W, CondenseGeom<NR>::lo(W), 0, 0>(acc, put);
+    else if constexpr (W + 1 < CondenseGeom<NR>::NW) wave_put<NR, W + 1>(w, acc, put);
+}
+
+template <int NR>
+__global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst C, int B, const double* __restrict__ X,
+                                                  const double* __restrict__ U, const double* __restrict__ AB,
+                                                  const double* __restrict__ DEF, double* __restrict__ Hs,
+                                                  double* __restrict__ hs, double* __restrict__ Cr,
+                                                  double* __restrict__ cl, double* __restrict__ cu,
+                                                  double* __restrict__ hmax, int tiled, double* __restrict__ Htl,
+                                                  double* __restrict__ Hab, double* __restrict__ Hbb) {
+    using Gm = CondenseGeom<NR>;
+    constexpr int WLDc = Gm::WLD;
+    constexpr int NT = 64 * Gm::NW;
     __shared__ double sA[NK * 16 + NK + 3];
-    __shared__ double Wc[16 * WLD];
+    __shared__ double Wc[16 * WLDc];
+    __shared__ double sG[4];
+    __shared__ double sMax[4];
     const int b = blockIdx.x;
-    const int l = threadIdx.x;
+    const int t = threadIdx.x;
+    const int l = t & 63, w = t >> 6;
     const int N = C.N, n = C.n;
     const double* Xb = X + (size_t)b * (N + 1) * NX;
     const double* Ub = U + (size_t)b * N * NU;
     const double* ABb = AB + (size_t)b * N * NK * 16;
     const double* DEFb = DEF + (size_t)b * N * NK;
 
-    for (int i = l; i < 16 * WLD; i += 64) Wc[i] = 0.0;
+    for (int i = t; i < 16 * WLDc; i += NT) Wc[i] = 0.0;
+    if (t < 4) sG[t] = 0.0;
 
-    const bool kite_lane = l < 3 * N;
-    const bool aff_lane = (l == 3 * N);
-    const int kb = l / 3, cc = l % 3;
+    const bool kite_lane = t < 3 * N;
+    const bool aff_lane = (t == 3 * N);
+    const int kb = t / 3, cc = t % 3;
     const double Dl = kite_lane ? 1.0 / C.Su[cc] : 0.0;
     double v[NK];
 #pragma unroll
     for (int i = 0; i < NK; ++i) v[i] = 0.0;
 
-    double4v acc[NTILE];
+    double4v acc[Gm::ACC];
 #pragma unroll
-    for (int t = 0; t < NTILE; ++t) acc[t] = double4v{0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < Gm::ACC; ++q) acc[q] = double4v{0.0, 0.0, 0.0, 0.0};
 
-    // software prefetch of interval data (221 doubles -> <= 4 per lane)
-    double pf[4];
+    // software prefetch of interval data (221 doubles -> <= 4 per thread)
+    constexpr int NPF = (NK * 16 + NK + NT - 1) / NT;
+    double pf[NPF];
 #define KITE_LOAD_INTERVAL(k)                                                              \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                        \
-        const int e = l + 64 * q;                                                          \
+    _Pragma("unroll") for (int q = 0; q < NPF; ++q) {                                      \
+        const int e = t + NT * q;                                                          \
         double val = 0.0;                                                                  \
         if (e < NK * 16) val = ABb[(size_t)(k) * NK * 16 + e];                             \
         else if (e < NK * 16 + NK) val = DEFb[(size_t)(k) * NK + (e - NK * 16)];           \
@@ -403,58 +491,58 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
     if (N > 0) { KITE_LOAD_INTERVAL(0) }
     __syncthreads();
 
+    // residual row weights in registers: stage sqrt(dt Q) Sr, Mayer sqrt(Q) Sr
+    double wpD[3], wpT[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { wpD[a] = C.sqQ_dt[a] * C.Sr[a]; wpT[a] = C.sqQ_T[a] * C.Sr[a]; }
     for (int k = 0; k <= N; ++k) {
         const bool last = (k == N);
         const double* xk = Xb + k * NX;
         const double th = xk[13], thd = xk[14];
         double Pp[3], dP[3];
         path_eval(C, th, Pp, dP);
-        // affine column (lane 3N) values broadcast
-        const double g0 = readlane_d(v[0], 3 * N);
-        const double g6 = readlane_d(v[6], 3 * N);
-        const double g7 = readlane_d(v[7], 3 * N);
-        const double g8 = readlane_d(v[8], 3 * N);
-        const double gr[3] = {g6, g7, g8};
+        const double g0 = sG[0];
+        const double gr[3] = {sG[1], sG[2], sG[3]};
         double wp[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) wp[a] = (last ? C.sqQ_T[a] : C.sqQ_dt[a]) * C.Sr[a];
+        for (int a = 0; a < 3; ++a) wp[a] = last ? wpT[a] : wpD[a];
         const double wv = last ? 0.0 : C.sw * C.sv;
         const int row0 = 4 * (k & 3);
 
         // kite columns: path rows -sq sr G[6+a], speed row 0
         if (kite_lane) {
-            Wc[(row0 + 0) * WLD + l] = -wp[0] * v[6];
-            Wc[(row0 + 1) * WLD + l] = -wp[1] * v[7];
-            Wc[(row0 + 2) * WLD + l] = -wp[2] * v[8];
-            Wc[(row0 + 3) * WLD + l] = 0.0;
+            Wc[(row0 + 0) * WLDc + t] = -wp[0] * v[6];
+            Wc[(row0 + 1) * WLDc + t] = -wp[1] * v[7];
+            Wc[(row0 + 2) * WLDc + t] = -wp[2] * v[8];
+            Wc[(row0 + 3) * WLDc + t] = 0.0;
         }
         // analytic columns 3N .. n (Uv_m, theta0, thetadot0, affine)
-        if (l < N + 3) {
-            const int col = 3 * N + l;
+        if (t < N + 3) {
+            const int col = 3 * N + t;
             double cth = 0.0, cthd = 0.0;
-            if (l < N) {
-                if (k > l) { cth = C.dt * C.dt * ((double)(k - l) - 0.5); cthd = C.dt; }
-            } else if (l == N) {
+            if (t < N) {
+                if (k > t) { cth = C.dt * C.dt * ((double)(k - t) - 0.5); cthd = C.dt; }
+            } else if (t == N) {
                 cth = 1.0;
-            } else if (l == N + 1) {
+            } else if (t == N + 1) {
                 cth = (double)k * C.dt; cthd = 1.0;
             }
-            if (l < N + 2) {
+            if (t < N + 2) {
 #pragma unroll
-                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLD + col] = wp[a] * dP[a] * cth;
-                Wc[(row0 + 3) * WLD + col] = -wv * cthd;
+                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLDc + col] = wp[a] * dP[a] * cth;
+                Wc[(row0 + 3) * WLDc + col] = -wv * cthd;
             } else {
 #pragma unroll
-                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLD + col] = wp[a] * (Pp[a] - xk[6 + a] - gr[a]);
-                Wc[(row0 + 3) * WLD + col] = last ? 0.0 : C.sw * (C.sv * C.vref - C.sv * thd);
+                for (int a = 0; a < 3; ++a) Wc[(row0 + a) * WLDc + col] = wp[a] * (Pp[a] - xk[6 + a] - gr[a]);
+                Wc[(row0 + 3) * WLDc + col] = last ? 0.0 : C.sw * (C.sv * C.vref - C.sv * thd);
             }
         }
         // vx bound rows (node k >= 1)
         if (k >= 1) {
             double* crow = Cr + ((size_t)b * N + (k - 1)) * n;
-            if (kite_lane) crow[l] = v[0] * Dl;
-            if (l < N + 2) crow[3 * N + l] = 0.0;
-            if (l == 0) {
+            if (kite_lane) crow[t] = v[0] * Dl;
+            if (t < N + 2) crow[3 * N + t] = 0.0;
+            if (t == 0) {
                 const double base = xk[0] + g0;
                 cl[(size_t)b * N + k - 1] = C.lo_fin ? (C.lbx[0] - base) : -INFINITY;
                 cu[(size_t)b * N + k - 1] = C.hi_fin ? (C.ubx[0] - base) : INFINITY;
@@ -463,24 +551,17 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
         if (last) {
             // zero the rows of nodes beyond N in this chunk
             for (int r = row0 + 4; r < 16; ++r)
-                for (int cidx = l; cidx <= n; cidx += 64) Wc[r * WLD + cidx] = 0.0;
+                for (int cidx = t; cidx <= n; cidx += NT) Wc[r * WLDc + cidx] = 0.0;
         }
         if ((k & 3) == 3 || last) {
             __syncthreads();
+            // fold the chunk: every wave into the tiles of its own tile rows
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                double fr[6];
+                double fr[NR];
 #pragma unroll
-                for (int I = 0; I < 6; ++I) fr[I] = Wc[(4 * s + (l >> 4)) * WLD + 16 * I + (l & 15)];
-                int t = 0;
-#pragma unroll
-                for (int I = 0; I < 6; ++I) {
-#pragma unroll
-                    for (int J = 0; J <= I; ++J) {
-                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[I], fr[J], acc[t], 0, 0, 0);
-                        ++t;
-                    }
-                }
+                for (int I = 0; I < NR; ++I) fr[I] = Wc[(4 * s + (l >> 4)) * WLDc + 16 * I + (l & 15)];
+                wave_fold<NR, 0>(w, acc, fr);
             }
             __syncthreads();
         }
@@ -488,8 +569,8 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
 
         // propagate G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = l + 64 * q;
+        for (int q = 0; q < NPF; ++q) {
+            const int e = t + NT * q;
             if (e < NK * 16 + NK) sA[e] = pf[q];
         }
         __syncthreads();
@@ -502,76 +583,65 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
             } else {
 #pragma unroll
                 for (int i = 0; i < NK; ++i) {
-                    double t = aff_lane ? sA[NK * 16 + i] : 0.0;
+                    double tt = aff_lane ? sA[NK * 16 + i] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NK; ++j) t = fma(sA[i * 16 + j], v[j], t);
-                    nv[i] = t;
+                    for (int j = 0; j < NK; ++j) tt = fma(sA[i * 16 + j], v[j], tt);
+                    nv[i] = tt;
                 }
             }
 #pragma unroll
             for (int i = 0; i < NK; ++i) v[i] = nv[i];
         }
         __syncthreads();
+        if (aff_lane) { sG[0] = v[0]; sG[1] = v[6]; sG[2] = v[7]; sG[3] = v[8]; }
+        __syncthreads();
     }
+#undef KITE_LOAD_INTERVAL
 
     // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar).
-    // tiled != 0 (k_qp_tiled): the control block H_aa (na = 4N = 16*NTA) goes
-    // out as C-layout tiles in lane order [tile][reg][lane], the theta
+    // tiled != 0 (k_qp_tiled, N = 20): the control block H_aa (na = 4N = 16*NTA)
+    // goes out as C-layout tiles in lane order [tile][reg][lane], the theta
     // couplings as H_ab [na][2] and H_bb [2][2]; otherwise the full n x n H.
     double* Hb = Hs + (size_t)b * n * n;
     const int na = 4 * N;
     double lmax = 0.0;
-    // scaled value of accumulator element (tile (I,J), reg r) or NaN if outside n x n
-    auto hval = [&](int I, int J, int r, double a, int& gi, int& gj) -> double {
-        gi = 16 * I + (l >> 4) + 4 * r;
-        gj = 16 * J + (l & 15);
-        double hv = a;
-        if (gi == gj) hv += col_rdiag(C, gi);
-        return hv * col_scale(C, gi) * col_scale(C, gj);
+    const ColConst K = col_const(C);
+    auto put = [&](int I, int J, double4v a4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gi = 16 * I + (l >> 4) + 4 * r;
+            const int gj = 16 * J + (l & 15);
+            const double a = a4[r];
+            if (gi < n && gj < n) {
+                double hv = a;
+                if (gi == gj) hv += col_rdiag(K, gi);
+                hv *= col_scale(K, gi) * col_scale(K, gj);
+                if (tiled) {
+                    if (gi < na) Htl[((size_t)b * QP_NTILE + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
+                    else if (gj < na) Hab[((size_t)b * na + gj) * 2 + (gi - na)] = hv;
+                    else {
+                        Hbb[(size_t)b * 4 + (gi - na) * 2 + (gj - na)] = hv;
+                        Hbb[(size_t)b * 4 + (gj - na) * 2 + (gi - na)] = hv;
+                    }
+                } else {
+                    Hb[(size_t)gi * n + gj] = hv;
+                    Hb[(size_t)gj * n + gi] = hv;
+                }
+                lmax = fmax(lmax, fabs(hv));
+            } else if (gi == n && gj < n) {
+                hs[(size_t)b * n + gj] = (a + col_rdiag(K, gj) * col_ubar(C, Ub, gj)) * col_scale(K, gj);
+            }
+        }
     };
-    if (tiled) {
-#pragma unroll
-        for (int I = 0; I < 6; ++I)
-#pragma unroll
-            for (int J = 0; J <= I; ++J)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int gi, gj;
-                    const double a = acc[I * (I + 1) / 2 + J][r];
-                    const double hv = hval(I, J, r, a, gi, gj);
-                    if (gi < n && gj < n) {
-                        if (gi < na) Htl[((size_t)b * QP_NTILE + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
-                        else if (gj < na) Hab[((size_t)b * na + gj) * 2 + (gi - na)] = hv;
-                        else {
-                            Hbb[(size_t)b * 4 + (gi - na) * 2 + (gj - na)] = hv;
-                            Hbb[(size_t)b * 4 + (gj - na) * 2 + (gi - na)] = hv;
-                        }
-                        lmax = fmax(lmax, fabs(hv));
-                    } else if (gi == n && gj < n) {
-                        hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
-                    }
-                }
-    } else {
-#pragma unroll
-        for (int I = 0; I < 6; ++I)
-#pragma unroll
-            for (int J = 0; J <= I; ++J)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    int gi, gj;
-                    const double a = acc[I * (I + 1) / 2 + J][r];
-                    const double hv = hval(I, J, r, a, gi, gj);
-                    if (gi < n && gj < n) {
-                        Hb[(size_t)gi * n + gj] = hv;
-                        Hb[(size_t)gj * n + gi] = hv;
-                        lmax = fmax(lmax, fabs(hv));
-                    } else if (gi == n && gj < n) {
-                        hs[(size_t)b * n + gj] = (a + col_rdiag(C, gj) * col_ubar(C, Ub, gj)) * col_scale(C, gj);
-                    }
-                }
-    }
+    wave_put<NR, 0>(w, acc, put);
     lmax = wave_max(lmax);
-    if (l == 0) hmax[b] = lmax;
+    if (l == 0) sMax[w] = lmax;
+    __syncthreads();
+    if (t == 0) {
+        double m = sMax[0];
+        for (int i = 1; i < Gm::NW; ++i) m = fmax(m, sMax[i]);
+        hmax[b] = m;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -586,7 +656,8 @@ __global__ __launch_bounds__(64) void k_condense(RtiConst C, int B, const double
 // Expansion dx_{k+1} = A_k dx_k + B_k du_k + d_k (theta rows exact), trajectory
 // and control update, diagnostics (kiteNMPF.cpp:319-355) and status.  One
 // wavefront; w = scaled QP step in slots (i = l + 64 s); vec/col: LDS scratch.
-__device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[2], double kkt, int iters,
+template <int NS>
+__device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[NS], double kkt, int iters,
                              const double* __restrict__ AB, const double* __restrict__ DEF,
                              double* __restrict__ Xb, double* __restrict__ Ub, double* __restrict__ u0_out,
                              double* __restrict__ diag, int32_t* __restrict__ status,
@@ -600,7 +671,7 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     // physical step dw = D w_s into vec
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const int i = l + 64 * s;
         if (i < n) vec[i] = accept ? w[s] * col_scale(C, i) : 0.0;
     }
@@ -696,8 +767,6 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     }
 }
 
-constexpr int NMAX = 4 * KITE_NMAX + 2;                 // 82
-constexpr int NPACK = NMAX * (NMAX + 1) / 2;             // 3403
 constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
 // Cholesky pivot safeguard (Wright 1999, see oracle/kite_oracle.cpp chol): a
 // pivot <= 0 from rounding near convergence is replaced by a huge value,
@@ -715,14 +784,27 @@ __device__ __forceinline__ int tri_row(int e) {
     return r;
 }
 
+// variable k of a slot vector (i = l + 64 s), broadcast to the wave
+template <int NS>
+__device__ __forceinline__ double slot_pivot(double x[NS], int k, int l) {
+    double v = x[0];
+#pragma unroll
+    for (int s = 1; s < NS; ++s) v = (k >= 64 * s) ? x[s] : v;
+    return readlane_d(v, k & 63);
+}
+
+template <int NS>
 struct QPState {
-    // per-lane slots: variable i = l + 64*s (s = 0,1)
-    double w[2], lb[2], ub[2], h[2], sl[2], zl[2], su[2], zu[2];
-    double rd[2], rpl[2], rpu[2];
+    // per-lane slots: variable i = l + 64*s (s = 0 .. NS-1)
+    double w[NS], lb[NS], ub[NS], h[NS], sl[NS], zl[NS], su[NS], zu[NS];
+    double rd[NS], rpl[NS], rpu[NS];
     // general rows: lane k < N
     double clo, chi, slo, zlo, shi, zhi, rplo, rphi, cw;
 };
 
+// NQ: largest n = 4N + 2 of the instantiation (82: N <= 20, 162: N <= 40);
+// C (vx-bound rows) is stored on its 3N kite columns only.
+template <int NQ>
 __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                                            const double* __restrict__ Hs, const double* __restrict__ hs,
                                            const double* __restrict__ Cr, const double* __restrict__ clp,
@@ -732,11 +814,13 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                                            double* __restrict__ u0_out, double* __restrict__ diag,
                                            int32_t* __restrict__ status, double* __restrict__ kkt_out,
                                            int32_t* __restrict__ iters_out) {
-    __shared__ double Lp[NPACK];
-    __shared__ double sC[KITE_NMAX * NMAX];
-    __shared__ double vec[NMAX + 2];
-    __shared__ double col[NMAX];
-    __shared__ double dinv[NMAX];
+    constexpr int NS = (NQ + 63) / 64;                 // variable slots per lane
+    constexpr int NQN = (NQ - 2) / 4;                  // largest horizon
+    __shared__ double Lp[NQ * (NQ + 1) / 2];
+    __shared__ double sC[NQN * 3 * NQN];
+    __shared__ double vec[NQ + 2];
+    __shared__ double col[NQ];
+    __shared__ double dinv[NQ];
 
     const int b = blockIdx.x;
     const int l = threadIdx.x;
@@ -746,14 +830,15 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     double* Xb = X + (size_t)b * (N + 1) * NX;
     double* Ub = U + (size_t)b * N * NU;
 
-    for (int e = l; e < N * n; e += 64) sC[e] = Crb[e];
+    const int nc = 3 * N;                             // C columns kept (kite controls)
+    for (int e = l; e < N * nc; e += 64) sC[e] = Crb[(e / nc) * n + e % nc];
 
-    QPState q;
+    QPState<NS> q;
     const bool has_lo = C.lo_fin != 0, has_hi = C.hi_fin != 0;
     const int nI = 2 * n + N * ((has_lo ? 1 : 0) + (has_hi ? 1 : 0));
     const bool row_lane = l < N;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const int i = l + 64 * s;
         double lo = 0.0, hi = 0.0, hv = 0.0;
         if (i < n) {
@@ -791,25 +876,26 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     auto rows_times = [&]() -> double {
         double t = 0.0;
         if (row_lane) {
-            const double* cr = sC + l * n;
-            for (int j = 0; j < n; ++j) t = fma(cr[j], vec[j], t);
+            const double* cr = sC + l * nc;
+            for (int j = 0; j < nc; ++j) t = fma(cr[j], vec[j], t);
         }
         return t;
     };
     // out_s = C^T y (y given in vec[] for rows)
-    auto rows_T = [&](double out[2]) {
+    auto rows_T = [&](double out[NS]) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int i = l + 64 * s;
             double t = 0.0;
             if (i < n)
-                for (int k = 0; k < N; ++k) t = fma(sC[k * n + i], vec[k], t);
+                if (i < nc)
+                    for (int k = 0; k < N; ++k) t = fma(sC[k * nc + i], vec[k], t);
             out[s] = t;
         }
     };
-    auto put_vec2 = [&](const double a[2]) {
+    auto put_vec2 = [&](const double a[NS]) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) { const int i = l + 64 * s; if (i < n) vec[i] = a[s]; }
+        for (int s = 0; s < NS; ++s) { const int i = l + 64 * s; if (i < n) vec[i] = a[s]; }
     };
 
     // initial slacks of general rows
@@ -827,23 +913,26 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         // vec <- w ; Hw (column sweep, H symmetric), Cw
         put_vec2(q.w);
         __syncthreads();
-        double hw[2] = {0.0, 0.0};
+        double hw[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) hw[s] = 0.0;
         for (int j = 0; j < n; ++j) {
             const double wj = vec[j];
             const double* hr = Hb + (size_t)j * n;
-            hw[0] = fma(hr[l < n ? l : 0], wj, hw[0]);
-            if (l + 64 < n) hw[1] = fma(hr[l + 64], wj, hw[1]);
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                if (l + 64 * s < n) hw[s] = fma(hr[l + 64 * s], wj, hw[s]);
         }
         q.cw = rows_times();
         __syncthreads();
         if (row_lane) vec[l] = (has_lo ? q.zlo : 0.0) - (has_hi ? q.zhi : 0.0);
         __syncthreads();
-        double ctz[2];
+        double ctz[NS];
         rows_T(ctz);
         __syncthreads();
         double rmax = 0.0, mu = 0.0;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int i = l + 64 * s;
             if (i < n) {
                 q.rd[s] = hw[s] + q.h[s] - (q.zl[s] - q.zu[s]) - ctz[s];
@@ -893,33 +982,37 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         }
     };
     // x <- M^-1 x with x in per-lane slots (2)
-    auto chol_solve = [&](double x[2]) {
+    auto chol_solve = [&](double x[NS]) {
         for (int k = 0; k < n; ++k) {
             double xk;
-            if (k < 64) { xk = readlane_d(x[0], k) * dinv[k]; if (l == k) x[0] = xk; }
-            else { xk = readlane_d(x[1], k - 64) * dinv[k]; if (l == k - 64) x[1] = xk; }
+            xk = slot_pivot<NS>(x, k, l) * dinv[k];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < NS; ++s)
+                if (l + 64 * s == k) x[s] = xk;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
                 const int i = l + 64 * s;
                 if (i > k && i < n) x[s] = fma(-Lp[pk(i, k)], xk, x[s]);
             }
         }
         for (int k = n - 1; k >= 0; --k) {
             double xk;
-            if (k < 64) { xk = readlane_d(x[0], k) * dinv[k]; if (l == k) x[0] = xk; }
-            else { xk = readlane_d(x[1], k - 64) * dinv[k]; if (l == k - 64) x[1] = xk; }
+            xk = slot_pivot<NS>(x, k, l) * dinv[k];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < NS; ++s)
+                if (l + 64 * s == k) x[s] = xk;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
                 const int i = l + 64 * s;
                 if (i < k) x[s] = fma(-Lp[pk(k, i)], xk, x[s]);
             }
         }
     };
 
-    double sgl[2], sgu[2], sglo = 0.0, sghi = 0.0;
+    double sgl[NS], sgu[NS], sglo = 0.0, sghi = 0.0;
     // Newton solve for complementarity rhs rc; returns directions
-    struct Dir { double dw[2], dsl[2], dsu[2], dzl[2], dzu[2], dslo, dshi, dzlo, dzhi; };
-    auto newton = [&](const double rcl[2], const double rcu[2], double rclo, double rchi, Dir& D) {
+    struct Dir { double dw[NS], dsl[NS], dsu[NS], dzl[NS], dzu[NS], dslo, dshi, dzlo, dzhi; };
+    auto newton = [&](const double rcl[NS], const double rcu[NS], double rclo, double rchi, Dir& D) {
         double t_lo = 0.0, t_hi = 0.0;
         if (row_lane) {
             if (has_lo) t_lo = rclo / q.slo - sglo * q.rplo;
@@ -928,11 +1021,11 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         __syncthreads();
         if (row_lane) vec[l] = t_lo - t_hi;
         __syncthreads();
-        double ct[2];
+        double ct[NS];
         rows_T(ct);
-        double r[2];
+        double r[NS];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int i = l + 64 * s;
             if (i < n) {
                 const double tl = rcl[s] / q.sl[s] - sgl[s] * q.rpl[s];
@@ -948,7 +1041,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         __syncthreads();
         const double cdw = rows_times();
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             D.dw[s] = r[s];
             D.dsl[s] = r[s] + q.rpl[s];
             D.dsu[s] = -r[s] + q.rpu[s];
@@ -964,7 +1057,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     auto max_step = [&](const Dir& D) -> double {
         double a = 1.0;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int i = l + 64 * s;
             if (i < n) {
                 if (D.dsl[s] < 0.0) a = fmin(a, -q.sl[s] / D.dsl[s]);
@@ -992,7 +1085,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         if (resid < IPM_FREEZE || resid != resid) { iters = it; break; }   // converged, or poisoned
         // sigma = z/s and the normal matrix H + A' Sigma A into Lp
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             sgl[s] = q.zl[s] / q.sl[s];
             sgu[s] = q.zu[s] / q.su[s];
         }
@@ -1004,11 +1097,12 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         for (int rr = 0; rr < n; ++rr) {
             const double* hr = Hb + (size_t)rr * n;
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            for (int s = 0; s < NS; ++s) {
                 const int c = l + 64 * s;
                 if (c <= rr) {
                     double m = hr[c];
-                    for (int k = 0; k < N; ++k) m = fma(sC[k * n + rr] * vec[k], sC[k * n + c], m);
+                    if (rr < nc && c < nc)
+                        for (int k = 0; k < N; ++k) m = fma(sC[k * nc + rr] * vec[k], sC[k * nc + c], m);
                     if (c == rr) m += sgl[s] + sgu[s];
                     Lp[pk(rr, c)] = m;
                 }
@@ -1017,16 +1111,16 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         __syncthreads();
         cholesky();
         // predictor
-        double rcl[2], rcu[2];
+        double rcl[NS], rcu[NS];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) { rcl[s] = -q.sl[s] * q.zl[s]; rcu[s] = -q.su[s] * q.zu[s]; }
+        for (int s = 0; s < NS; ++s) { rcl[s] = -q.sl[s] * q.zl[s]; rcu[s] = -q.su[s] * q.zu[s]; }
         double rclo = -q.slo * q.zlo, rchi = -q.shi * q.zhi;
         Dir Da;
         newton(rcl, rcu, rclo, rchi, Da);
         const double aa = max_step(Da);
         double mua = 0.0;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int i = l + 64 * s;
             if (i < n)
                 mua += (q.sl[s] + aa * Da.dsl[s]) * (q.zl[s] + aa * Da.dzl[s]) +
@@ -1041,7 +1135,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         sigma = sigma * sigma * sigma;
         // corrector
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             rcl[s] = -q.sl[s] * q.zl[s] - Da.dsl[s] * Da.dzl[s] + sigma * mu;
             rcu[s] = -q.su[s] * q.zu[s] - Da.dsu[s] * Da.dzu[s] + sigma * mu;
         }
@@ -1051,7 +1145,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         newton(rcl, rcu, rclo, rchi, Dc);
         const double a = fmin(1.0, IPM_TAU * max_step(Dc));
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < NS; ++s) {
             q.w[s] += a * Dc.dw[s];
             q.sl[s] += a * Dc.dsl[s]; q.su[s] += a * Dc.dsu[s];
             q.zl[s] += a * Dc.dzl[s]; q.zu[s] += a * Dc.dzu[s];
@@ -1065,7 +1159,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     residuals();
     const double kkt = resid;
 
-    rti_epilogue(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out, vec, col);
+    rti_epilogue<NS>(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out, vec, col);
 }
 
 // ---------------------------------------------------------------------------
@@ -1180,16 +1274,33 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
                            const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
                            double* hmax, int tiled, double* Htl, double* Hab, double* Hbb, hipStream_t s) {
-    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), 0, s, C, B, X, U, AB, DEF, Hs, hs, Cr, cl, cu, hmax,
-                       tiled, Htl, Hab, Hbb);
+    const int NR = (C.n + 1 + 15) / 16;
+#define KITE_CONDENSE(R)                                                                                    \
+    case R:                                                                                                 \
+        hipLaunchKernelGGL(k_condense<R>, dim3(B), dim3(64 * CondenseGeom<R>::NW), 0, s, C, B, X, U, AB, DEF, \
+                           Hs, hs, Cr, cl, cu,                                                              \
+                           hmax, tiled, Htl, Hab, Hbb);                                                     \
+        break;
+    switch (NR) {
+        KITE_CONDENSE(1) KITE_CONDENSE(2) KITE_CONDENSE(3) KITE_CONDENSE(4) KITE_CONDENSE(5) KITE_CONDENSE(6)
+        KITE_CONDENSE(7) KITE_CONDENSE(8) KITE_CONDENSE(9) KITE_CONDENSE(10) KITE_CONDENSE(11)
+        default: return hipErrorInvalidValue;
+    }
+#undef KITE_CONDENSE
     return hipGetLastError();
 }
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
                      int32_t* status, double* kkt, int32_t* iters, hipStream_t s) {
-    hipLaunchKernelGGL(k_qp, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U, u0,
-                       diag, status, kkt, iters);
+    if (C.n <= 82)
+        hipLaunchKernelGGL(k_qp<82>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U, u0,
+                           diag, status, kkt, iters);
+    else if (C.n <= 162)
+        hipLaunchKernelGGL(k_qp<162>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U,
+                           u0, diag, status, kkt, iters);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,

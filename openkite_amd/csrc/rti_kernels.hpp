@@ -8,7 +8,7 @@
 
 // Largest horizon the fused condense/QP kernels are built for (LDS budget of
 // the wave-per-instance QP).  n = 4N+2 <= 82 decision variables.
-#define KITE_NMAX 20
+#define KITE_NMAX 40
 
 namespace kite {
 

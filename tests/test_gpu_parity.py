@@ -312,6 +312,27 @@ def test_qp_kernels_vs_oracle(kp, cfgv, qp_kernel):
         g.close()
 
 
+@pytest.mark.parametrize("Nh", [8, 16, 40])
+def test_rti_horizons_vs_oracle(kp, Nh):
+    """Other horizons: condensing with 3 / 5 / 11 tile rows and 1-4 waves, the
+    wave-scalar QP for n <= 82 and n = 162 (N = 40: BASELINE config 5)."""
+    B = 8
+    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    x = x0_batch(B, offset=6000)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(N=Nh), B)
+    Xo = np.zeros((B, Nh + 1, 15)); Uo = np.zeros((B, Nh, 4))
+    try:
+        for step in range(3):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            assert e < RTI_TOL, (Nh, step, e)
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+
+
 def test_step_device_on_torch_stream_matches_host_step():
     """Device-pointer entry point on torch's default stream (handle 0 = HIP null
     stream), closed loop on the device, bitwise equal to the host entry point."""
