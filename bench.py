@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--qp-iters", type=int, default=16)
     ap.add_argument("--qp-kernel", type=int, default=0, help="0 auto, 1 wave-scalar, 2 MFMA-tiled")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--ekf", action="store_true",
+                    help="fuse the EKF estimate (kiteEKF.cpp) before every RTI step (BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     return ap.parse_args()
@@ -151,9 +153,31 @@ def main():
     d_status = torch.zeros((B,), dtype=torch.int32, device=dev)
     pub = Publisher(B, dev, world) if world > 1 and not args.no_allgather else None
 
+    if args.ekf:
+        W, V, P0 = ok.ekf_default_covariances()
+        d_W = torch.from_numpy(W).to(dev); d_V = torch.from_numpy(V).to(dev)
+        d_P = torch.from_numpy(np.repeat(P0[None], B, axis=0)).to(dev)
+        d_xe = d_x0[:, :13].clone()
+        d_u3 = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+        d_z = d_x0[:, 6:13].clone()
+
     def one_step():
+        if args.ekf:
+            # estimator (kiteEKF.cpp:75-126): propagate under the applied control,
+            # update with the measured position + attitude of the plant (here the
+            # model's own prediction), then the RTI from the estimate
+            # (propagation in 5 steps of dt/5: one RK4 step of 0.05 s is too coarse
+            # for the tether dynamics; the reference estimator runs at the
+            # measurement rate)
+            d_u3.copy_(d_u0[:, :3])
+            for j in range(5):
+                ctx.ekf_step_device(B, cfg.dt / 5, d_xe.data_ptr(), d_u3.data_ptr(), d_P.data_ptr(),
+                                    d_z.data_ptr() if j == 4 else 0, d_W.data_ptr(), d_V.data_ptr())
+            d_x0[:, :13].copy_(d_xe)
         ctx.step_device(d_x0.data_ptr(), d_u0.data_ptr(), d_traj.data_ptr(), 0, d_diag.data_ptr(),
                         d_status.data_ptr())
+        if args.ekf:
+            d_z.copy_(d_traj[:, 1, 6:13])
         if pub is not None:
             pub.publish(d_u0, d_diag)          # all ranks see every kite's u0 + diagnostics
         d_x0.copy_(d_traj[:, 1, :])        # closed loop: predicted state at t0 + dt
@@ -212,7 +236,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded perturbations of launch/simulator.launch:3, umx_radian params)",
-            "config": {"workload": f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64 (BASELINE configs[2])",
+            "config": {"workload": (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
+                                    + (" + fused EKF (BASELINE configs[4])" if args.ekf else
+                                       " (BASELINE configs[2])" if N == 20 else "")),
+                       "ekf": bool(args.ekf),
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
                        "allgather": bool(world > 1 and not args.no_allgather)},

@@ -257,6 +257,9 @@ __global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, in
 // accumulator live in LDS (SoA [component][lane], conflict-free, 312 B/lane;
 // 128-lane blocks -> 4 blocks = 8 waves per CU in 160 KiB).
 constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances x 16 dirs
+#ifndef KITE_RK_OCC
+#define KITE_RK_OCC 2                     // launch_bounds occupancy hint of k_rk4_sens
+#endif
 constexpr int RK_LDS = 3 * NK;            // x.v, x.t, acc.t
 __device__ __forceinline__ void rk4_dual(const ModelConst& P, Dual* x /*in/out [NK]*/, const Dual* u,
                                          double h, int M, double (*sh)[RK_T], int tid) {
@@ -291,7 +294,7 @@ __device__ __forceinline__ void rk4_dual(const ModelConst& P, Dual* x /*in/out [
     }
 }
 
-__global__ __launch_bounds__(RK_T, 2) void k_rk4_sens(ModelConst P, int B, int N, int M, double h,
+__global__ __launch_bounds__(RK_T, KITE_RK_OCC) void k_rk4_sens(ModelConst P, int B, int N, int M, double h,
                                                    const double* __restrict__ X,
                                                    const double* __restrict__ U,
                                                    double* __restrict__ AB,

@@ -346,6 +346,12 @@ class BatchNMPC:
         _check(lib().kite_nmpc_colloc_eval(self._h, ctypes.byref(cfg), c, _p(zz), _p(G), _p(J), _p(Jb)), "colloc_eval")
         return (G, J, Jb) if jac else (G, J)
 
+    def ekf_step_device(self, count: int, dt: float, d_x13: int, d_u3: int, d_P169: int, d_z7: int,
+                        d_W169: int, d_V49: int):
+        """Device-pointer EKF step (asynchronous on the context stream)."""
+        _check(lib().kite_nmpc_ekf_step_device(self._h, int(count), float(dt), d_x13, d_u3, d_P169, d_z7 or None,
+                                               d_W169, d_V49), "ekf_step_device")
+
     def ekf_step(self, x13, u3, P, dt: float, z7=None, W=None, V=None):
         """Batched KiteEKF propagate (+ update when z7 is given); returns (x, P)."""
         x = _f64(x13).reshape(-1, 13).copy()
