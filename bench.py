@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--qp-iters", type=int, default=16)
     ap.add_argument("--qp-kernel", type=int, default=0, help="0 auto, 1 wave-scalar, 2 MFMA-tiled")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--fp32-sens", action="store_true",
+                    help="RK4 + sensitivities in fp32, QP fp64 (BASELINE configs[3] mixed precision)")
     ap.add_argument("--ekf", action="store_true",
                     help="fuse the EKF estimate (kiteEKF.cpp) before every RTI step (BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -139,6 +141,7 @@ def main():
     B, N = args.batch, args.horizon
     cfg = ok.default_config(N=N, M=args.substeps, qp_iters=args.qp_iters, device=local)
     cfg.qp_kernel = args.qp_kernel
+    cfg.sens_fp32 = 1 if args.fp32_sens else 0
     ctx = ok.BatchNMPC(ok.load_properties(), cfg, B)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
@@ -234,9 +237,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if not args.fp32_sens else "f64 (f32 sensitivities)",
             "data": "synthetic (seeded perturbations of launch/simulator.launch:3, umx_radian params)",
             "config": {"workload": (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
+                                    + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
                                     + (" + fused EKF (BASELINE configs[4])" if args.ekf else
                                        " (BASELINE configs[2])" if N == 20 else "")),
                        "ekf": bool(args.ekf),

@@ -113,6 +113,9 @@ typedef struct kite_nmpc_config {
                              at node round(delay/dt).  0 = off: KiteNMPF semantics, the
                              caller passes the predicted state (default).  The node
                              uses 0.1 (nmpf_node.cpp:74).                              */
+    int32_t sens_fp32;    /* 1: RK4 + forward sensitivities in fp32 (mixed precision,
+                             BASELINE config 4); condensing, QP, expansion stay fp64 */
+    int32_t reserved;
 } kite_nmpc_config;
 
 /* ---- diagnostics: msg/mpc_diagnostic.msg (filled at nmpf_node.cpp:191-204) */

@@ -86,6 +86,43 @@ __device__ __forceinline__ Dual datan2(Dual y, Dual x, Dual r2) {
     return mk(atan2(y.v, x.v), (x.v * y.t - y.v * x.t) / r2.v);
 }
 
+// ---------------------------------------------------------------------------
+// Single-precision dual number (mixed-precision sensitivities, config
+// sens_fp32 = 1): value and tangent in fp32 (2x the fp64 VALU rate, half the
+// registers); model constants are rounded to fp32 at use.
+// ---------------------------------------------------------------------------
+struct DualF {
+    float v, t;
+    DualF() = default;
+    __host__ __device__ constexpr DualF(double a) : v((float)a), t(0.0f) {}
+    __host__ __device__ constexpr DualF(float a, float b) : v(a), t(b) {}
+};
+__device__ __forceinline__ DualF mkf(float v, float t) { return DualF(v, t); }
+__device__ __forceinline__ DualF operator+(DualF a, DualF b) { return mkf(a.v + b.v, a.t + b.t); }
+__device__ __forceinline__ DualF operator-(DualF a, DualF b) { return mkf(a.v - b.v, a.t - b.t); }
+__device__ __forceinline__ DualF operator-(DualF a) { return mkf(-a.v, -a.t); }
+__device__ __forceinline__ DualF operator*(DualF a, DualF b) { return mkf(a.v * b.v, fmaf(a.t, b.v, a.v * b.t)); }
+__device__ __forceinline__ DualF operator+(DualF a, double b) { return mkf(a.v + (float)b, a.t); }
+__device__ __forceinline__ DualF operator+(double b, DualF a) { return mkf(a.v + (float)b, a.t); }
+__device__ __forceinline__ DualF operator-(DualF a, double b) { return mkf(a.v - (float)b, a.t); }
+__device__ __forceinline__ DualF operator-(double b, DualF a) { return mkf((float)b - a.v, -a.t); }
+__device__ __forceinline__ DualF operator*(DualF a, double b) { const float f = (float)b; return mkf(a.v * f, a.t * f); }
+__device__ __forceinline__ DualF operator*(double b, DualF a) { const float f = (float)b; return mkf(a.v * f, a.t * f); }
+__device__ __forceinline__ DualF operator/(DualF a, DualF b) {
+    const float ib = 1.0f / b.v;
+    const float q = a.v * ib;
+    return mkf(q, (a.t - q * b.t) * ib);
+}
+__device__ __forceinline__ DualF operator/(DualF a, double b) { const float ib = (float)(1.0 / b); return mkf(a.v * ib, a.t * ib); }
+__device__ __forceinline__ DualF rcp(DualF a) { const float r = 1.0f / a.v; return mkf(r, -a.t * r * r); }
+__device__ __forceinline__ float val(DualF a) { return a.v; }
+__device__ __forceinline__ DualF dsqrt(DualF a) { const float s = sqrtf(a.v); return mkf(s, a.t * (0.5f / s)); }
+__device__ __forceinline__ DualF dexp(DualF a) { const float e = expf(a.v); return mkf(e, a.t * e); }
+__device__ __forceinline__ DualF dasin(DualF x, DualF cosv) { return mkf(asinf(x.v), x.t / cosv.v); }
+__device__ __forceinline__ DualF datan2(DualF y, DualF x, DualF r2) {
+    return mkf(atan2f(y.v, x.v), (x.v * y.t - y.v * x.t) / r2.v);
+}
+
 template <class T> struct V3 { T x, y, z; };
 
 template <class T>

@@ -120,6 +120,7 @@ RtiConst make_rti_const(const kite_nmpc_config& c) {
     r.delay = c.delay;
     r.delay_steps = c.delay_steps;
     r.delay_node = (int)std::lround(c.delay / c.dt);
+    r.sens_fp32 = c.sens_fp32;
     return r;
 }
 
@@ -137,6 +138,7 @@ int validate_config(const kite_nmpc_config& c) {
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
     if (c.qp_kernel < 0 || c.qp_kernel > 2) return KITE_EINVAL;
+    if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
     if (!(c.delay >= 0.0) || !std::isfinite(c.delay) || std::lround(c.delay / c.dt) > c.N) return KITE_EINVAL;
     if (c.delay > 0.0 && (c.delay_steps < 1 || c.delay_steps > 64)) return KITE_EINVAL;
     return KITE_OK;
@@ -304,6 +306,7 @@ void kite_nmpc_default_config(kite_nmpc_config* c) {
     const double inf = INFINITY, pi = M_PI;
     c->N = 20; c->M = 2; c->qp_iters = 16; c->shift = 1; c->device = 0; c->timing = 0;
     c->delay = 0.0; c->delay_steps = 4;
+    c->sens_fp32 = 0;
     c->dt = 0.05;
     const double Q[3] = {1e3, 1e3, 1e4};
     const double R[4] = {1e-4, 1e-1, 1e-1, 1e-3};

@@ -261,11 +261,13 @@ constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances
 #define KITE_RK_OCC 2                     // launch_bounds occupancy hint of k_rk4_sens
 #endif
 constexpr int RK_LDS = 3 * NK;            // x.v, x.t, acc.t
-__device__ __forceinline__ void rk4_dual(const ModelConst& P, Dual* x /*in/out [NK]*/, const Dual* u,
-                                         double h, int M, double (*sh)[RK_T], int tid) {
+// DT: dual number (Dual fp64 / DualF fp32 for config.sens_fp32), ST: its scalar
+template <class DT, class ST>
+__device__ __forceinline__ void rk4_dual(const ModelConst& P, DT* x /*in/out [NK]*/, const DT* u, ST h, int M,
+                                         ST (*sh)[RK_T], int tid) {
     for (int m = 0; m < M; ++m) {
-        Dual xs[NK], kv[NK];
-        double accv[NK];
+        DT xs[NK], kv[NK];
+        ST accv[NK];
 #pragma unroll
         for (int i = 0; i < NK; ++i) {
             sh[i][tid] = x[i].v;
@@ -278,49 +280,72 @@ __device__ __forceinline__ void rk4_dual(const ModelConst& P, Dual* x /*in/out [
         asm volatile("" ::: "memory");
 #pragma unroll 1
         for (int st = 0; st < 4; ++st) {
-            kite_rhs<Dual>(P, xs, u, kv);
-            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
-            const double wn = (st < 2) ? 0.5 * h : h;
+            kite_rhs<DT>(P, xs, u, kv);
+            const ST wa = (st == 0 || st == 3) ? h / ST(6) : h / ST(3);
+            const ST wn = (st < 2) ? ST(0.5) * h : h;
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
                 accv[i] = fma(wa, kv[i].v, accv[i]);
                 sh[2 * NK + i][tid] = fma(wa, kv[i].t, sh[2 * NK + i][tid]);
-                xs[i] = Dual(fma(wn, kv[i].v, sh[i][tid]), fma(wn, kv[i].t, sh[NK + i][tid]));
+                xs[i] = DT(fma(wn, kv[i].v, sh[i][tid]), fma(wn, kv[i].t, sh[NK + i][tid]));
             }
             asm volatile("" ::: "memory");
         }
 #pragma unroll
-        for (int i = 0; i < NK; ++i) x[i] = Dual(accv[i], sh[2 * NK + i][tid]);
+        for (int i = 0; i < NK; ++i) x[i] = DT(accv[i], sh[2 * NK + i][tid]);
     }
 }
 
+template <class DT, class ST>
 __global__ __launch_bounds__(RK_T, KITE_RK_OCC) void k_rk4_sens(ModelConst P, int B, int N, int M, double h,
-                                                   const double* __restrict__ X,
-                                                   const double* __restrict__ U,
-                                                   double* __restrict__ AB,
-                                                   double* __restrict__ DEF) {
-    __shared__ double xsh[RK_LDS][RK_T];
+                                                             const double* __restrict__ X,
+                                                             const double* __restrict__ U,
+                                                             double* __restrict__ AB,
+                                                             double* __restrict__ DEF) {
+    __shared__ ST xsh[RK_LDS][RK_T];
     const int d = threadIdx.x & 15;
     const int b = blockIdx.x * (RK_T / 16) + (threadIdx.x >> 4);
     const int k = blockIdx.y;
     if (b >= B) return;
     const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
     const double* uk = U + ((size_t)b * N + k) * NU;
-    Dual x[NK], u[NKU];
+    DT x[NK], u[NKU];
 #pragma unroll
-    for (int i = 0; i < NK; ++i) x[i] = mk(xk[i], d == i ? 1.0 : 0.0);
+    for (int i = 0; i < NK; ++i) x[i] = DT(ST(xk[i]), ST(d == i ? 1 : 0));
 #pragma unroll
-    for (int j = 0; j < NKU; ++j) u[j] = mk(uk[j], d == NK + j ? 1.0 : 0.0);
-    rk4_dual(P, x, u, h, M, xsh, threadIdx.x);
+    for (int j = 0; j < NKU; ++j) u[j] = DT(ST(uk[j]), ST(d == NK + j ? 1 : 0));
+    rk4_dual<DT, ST>(P, x, u, ST(h), M, xsh, threadIdx.x);
     double* ab = AB + ((size_t)b * N + k) * (NK * 16);
 #pragma unroll
-    for (int i = 0; i < NK; ++i) ab[i * 16 + d] = x[i].t;
+    for (int i = 0; i < NK; ++i) ab[i * 16 + d] = (double)x[i].t;
     if (d == 0) {
         const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
         double* df = DEF + ((size_t)b * N + k) * NK;
+        // mixed precision: the defects (the QP's right-hand side) come from
+        // the fp64 primal of k_defects; only the sensitivities are fp32 here
+        if constexpr (std::is_same<ST, double>::value) {
 #pragma unroll
-        for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+            for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+        }
     }
+}
+
+// fp64 multiple-shooting defects x+(x_k, u_k) - x_{k+1}, lane per (instance,
+// interval): the right-hand side of the QP when the sensitivities run in fp32
+__global__ __launch_bounds__(64, 2) void k_defects(ModelConst P, int B, int N, int M, double h,
+                                                 const double* __restrict__ X, const double* __restrict__ U,
+                                                 double* __restrict__ DEF) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= B * N) return;
+    const int b = g / N, k = g % N;
+    const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
+    const double* uk = U + ((size_t)b * N + k) * NU;
+    double x0[NX], u4[NU], xo[NX];
+    for (int i = 0; i < NX; ++i) x0[i] = xk[i];
+    for (int j = 0; j < NU; ++j) u4[j] = uk[j];
+    rk4_primal(P, x0, u4, h, M, xo);
+    double* df = DEF + ((size_t)b * N + k) * NK;
+    for (int i = 0; i < NK; ++i) df[i] = xo[i] - xk[NX + i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1271,7 +1296,13 @@ hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int wa
 }
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
                            double* AB, double* DEF, hipStream_t s) {
-    hipLaunchKernelGGL(k_rk4_sens, dim3((B + RK_T / 16 - 1) / (RK_T / 16), C.N), dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
+    const dim3 grid((B + RK_T / 16 - 1) / (RK_T / 16), C.N);
+    if (C.sens_fp32) {
+        hipLaunchKernelGGL((k_rk4_sens<DualF, float>), grid, dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
+        hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF);
+    }
+    else
+        hipLaunchKernelGGL((k_rk4_sens<Dual, double>), grid, dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
     return hipGetLastError();
 }
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,

@@ -54,6 +54,7 @@ class NmpcConfig(ctypes.Structure):
         ("vref", ctypes.c_double), ("path_radius", ctypes.c_double), ("path_altitude", ctypes.c_double),
         ("path_q", ctypes.c_double * 4), ("theta_flex", ctypes.c_double), ("min_speed", ctypes.c_double),
         ("delay", ctypes.c_double),
+        ("sens_fp32", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
     def to_dict(self) -> dict:

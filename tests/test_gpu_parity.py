@@ -333,6 +333,28 @@ def test_rti_horizons_vs_oracle(kp, Nh):
         g.close()
 
 
+def test_rti_fp32_sensitivities_vs_oracle(kp, cfgv):
+    """Mixed precision (config.sens_fp32 = 1, BASELINE config 4): RK4 and the
+    forward sensitivities in fp32, condensing / QP / expansion in fp64.  The
+    fp64 oracle is the reference; SURVEY 8(c) states 1e-4 for fp32 RTI u0."""
+    B = 16
+    x = x0_batch(B, offset=7000)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(sens_fp32=1), B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    worst = 0.0
+    try:
+        for step in range(4):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            worst = max(worst, e)
+            assert e < 1e-4, (step, e)
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+    print(f"fp32 sensitivities: worst RTI relative error vs fp64 oracle {worst:.2e}")
+
+
 def test_step_device_on_torch_stream_matches_host_step():
     """Device-pointer entry point on torch's default stream (handle 0 = HIP null
     stream), closed loop on the device, bitwise equal to the host entry point."""
