@@ -89,8 +89,9 @@ typedef struct kite_nmpc_config {
     int32_t shift;        /* 1: shift the warm start by one interval per step  */
     int32_t device;       /* HIP device ordinal                                 */
     int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
-    int32_t qp_kernel;    /* 0: auto (MFMA-tiled QP when N == 20), 1: wave-scalar LDS QP,
-                             2: MFMA-tiled (KITE_EINVAL unless N == 20) */
+    int32_t qp_kernel;    /* 0: auto (MFMA-tiled QP when N == 20 or 40), 1: wave-scalar LDS QP,
+                             2: MFMA-tiled (register tiles at N == 20, LDS tiles with
+                             4 waves per kite at N == 40; KITE_EINVAL otherwise) */
     int32_t delay_steps;  /* RK4 substeps of the delay-compensation prediction (4) */
     double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
     double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */

@@ -39,7 +39,8 @@ struct kite_nmpc_ctx {
     double *u0 = nullptr, *diag = nullptr, *kkt = nullptr;
     int32_t* status = nullptr;
     int32_t* iters = nullptr;
-    // tiled-QP layout (N == 20): H_aa tiles [B][15][4][64], H_ab [B][80][2], H_bb [B][2][2]
+    // tiled-QP layout (N == 20, 40): H_aa lower tiles [B][NT(NT+1)/2][4][64] with
+    // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     // scratch for the model-level entry points
@@ -358,13 +359,14 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     if (cfg->qp_kernel == 2 && !tiled_ok) { delete ctx; return KITE_EINVAL; }
     ctx->tiled = cfg->qp_kernel == 2 || (cfg->qp_kernel == 0 && tiled_ok);
     const size_t na = 4 * N;
+    const size_t ntile = (N / 4) * (N / 4 + 1) / 2;
     struct Alloc { double** p; size_t count; };
     const Alloc allocs[] = {
         {&ctx->X, B * (N + 1) * 15}, {&ctx->U, B * N * 4}, {&ctx->x0, B * 15},
         {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13}, {&ctx->Hs, ctx->tiled ? 1 : B * n * n},
         {&ctx->hs, B * n}, {&ctx->Cr, B * N * n}, {&ctx->cl, B * N}, {&ctx->cu, B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
-        {&ctx->Htl, ctx->tiled ? B * 15 * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
+        {&ctx->Htl, ctx->tiled ? B * ntile * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
         {&ctx->Hbb, ctx->tiled ? B * 4 : 1},
     };
     for (const Alloc& a : allocs) {
@@ -830,14 +832,14 @@ int kite_nmpc_get_qp(kite_nmpc_ctx* ctx, int32_t instance, double* H, double* h,
     if (H && ctx->tiled) {
         // reassemble the full matrix from the C-layout tiles (lane l: column l&15,
         // rows (l>>4) + 4r), H_ab and H_bb
-        const size_t na = 4 * N;
-        std::vector<double> tl(15 * 256), ab(na * 2), bb(4);
-        HIP_TRY(hipMemcpyAsync(tl.data(), ctx->Htl + b * 15 * 256, tl.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        const size_t na = 4 * N, nt = N / 4, ntile = nt * (nt + 1) / 2;
+        std::vector<double> tl(ntile * 256), ab(na * 2), bb(4);
+        HIP_TRY(hipMemcpyAsync(tl.data(), ctx->Htl + b * ntile * 256, tl.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(ab.data(), ctx->Hab + b * na * 2, ab.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(bb.data(), ctx->Hbb + b * 4, 4 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         int t = 0;
-        for (int I = 0; I < 5; ++I)
+        for (int I = 0; I < (int)nt; ++I)
             for (int J = 0; J <= I; ++J, ++t)
                 for (int r = 0; r < 4; ++r)
                     for (int l = 0; l < 64; ++l) {

@@ -627,11 +627,12 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
 #undef KITE_LOAD_INTERVAL
 
     // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar).
-    // tiled != 0 (k_qp_tiled, N = 20): the control block H_aa (na = 4N = 16*NTA)
+    // tiled != 0 (k_qp_tiled N = 20, k_qp_lds N = 40): the control block H_aa (na = 4N = 16*NT)
     // goes out as C-layout tiles in lane order [tile][reg][lane], the theta
     // couplings as H_ab [na][2] and H_bb [2][2]; otherwise the full n x n H.
     double* Hb = Hs + (size_t)b * n * n;
     const int na = 4 * N;
+    const int ntile = (N / 4) * (N / 4 + 1) / 2;       // tiled: lower tiles of H_aa (N % 4 == 0)
     double lmax = 0.0;
     const ColConst K = col_const(C);
     auto put = [&](int I, int J, double4v a4) {
@@ -645,7 +646,7 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
                 if (gi == gj) hv += col_rdiag(K, gi);
                 hv *= col_scale(K, gi) * col_scale(K, gj);
                 if (tiled) {
-                    if (gi < na) Htl[((size_t)b * QP_NTILE + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
+                    if (gi < na) Htl[((size_t)b * ntile + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
                     else if (gj < na) Hab[((size_t)b * na + gj) * 2 + (gi - na)] = hv;
                     else {
                         Hbb[(size_t)b * 4 + (gi - na) * 2 + (gj - na)] = hv;
@@ -684,7 +685,14 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
 // Expansion dx_{k+1} = A_k dx_k + B_k du_k + d_k (theta rows exact), trajectory
 // and control update, diagnostics (kiteNMPF.cpp:319-355) and status.  One
 // wavefront; w = scaled QP step in slots (i = l + 64 s); vec/col: LDS scratch.
-template <int NS>
+// WAVE: the caller is one wavefront of a larger block (the other waves have
+// left), so the LDS exchanges are ordered by a wavefront fence, not s_barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int NS, bool WAVE = false>
 __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[NS], double kkt, int iters,
                              const double* __restrict__ AB, const double* __restrict__ DEF,
                              double* __restrict__ Xb, double* __restrict__ Ub, double* __restrict__ u0_out,
@@ -697,13 +705,13 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     // contributes no step; the shifted plan is kept and the gaps are closed
     const bool accept = kkt < QP_STEP_ACCEPT;
     // physical step dw = D w_s into vec
-    __syncthreads();
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const int i = l + 64 * s;
         if (i < n) vec[i] = accept ? w[s] * col_scale(C, i) : 0.0;
     }
-    __syncthreads();
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
     const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
     // theta / thetadot rows (exact double integrator), lane = node
     for (int k = l; k <= N; k += 64) {
@@ -727,9 +735,9 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         const double* ABb = AB + (size_t)b * N * NK * 16;
         const double* DEFb = DEF + (size_t)b * N * NK;
         for (int k = 0; k < N; ++k) {
-            __syncthreads();
+            if constexpr (WAVE) wave_sync(); else __syncthreads();
             if (l < NK) col[l] = dx;
-            __syncthreads();
+            if constexpr (WAVE) wave_sync(); else __syncthreads();
             if (l < NK) {
                 const double* ar = ABb + ((size_t)k * NK + l) * 16;
                 double t = DEFb[(size_t)k * NK + l];
@@ -740,7 +748,7 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
             }
         }
     }
-    __syncthreads();
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
 
     // ---- diagnostics, cost, status -------------------------------------------
     double cost = 0.0;

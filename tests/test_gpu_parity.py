@@ -315,7 +315,8 @@ def test_qp_kernels_vs_oracle(kp, cfgv, qp_kernel):
 @pytest.mark.parametrize("Nh", [8, 16, 40])
 def test_rti_horizons_vs_oracle(kp, Nh):
     """Other horizons: condensing with 3 / 5 / 11 tile rows and 1-4 waves, the
-    wave-scalar QP for n <= 82 and n = 162 (N = 40: BASELINE config 5)."""
+    wave-scalar QP for n <= 82 and the LDS-tiled block QP at n = 162 (N = 40:
+    BASELINE config 5, auto kernel choice)."""
     B = 8
     cv = ffi.cfg_vector(ffi.node_config(N=Nh))
     x = x0_batch(B, offset=6000)
@@ -329,6 +330,43 @@ def test_rti_horizons_vs_oracle(kp, Nh):
             assert e < RTI_TOL, (Nh, step, e)
             np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
             x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("qp_kernel", [1, 2])
+def test_n40_qp_kernels_vs_oracle(kp, qp_kernel):
+    """N = 40 (BASELINE config 5): the wave-scalar QP (1) and the block-per-kite
+    LDS-tiled QP (2, k_qp_lds) against the oracle over 4 warm steps, plus the
+    tiled H layout reassembled by get_qp."""
+    B, Nh = 16, 40
+    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    x = x0_batch(B, offset=7000)
+    cfg = ok.default_config(N=Nh)
+    cfg.qp_kernel = qp_kernel
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    Xo = np.zeros((B, Nh + 1, 15)); Uo = np.zeros((B, Nh, 4))
+    try:
+        for step in range(4):
+            Xin, Uin = Xo.copy(), Uo.copy()
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            assert e < RTI_TOL, (qp_kernel, step, e)
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            if step == 0:
+                # condensed QP of the cold step vs the oracle (tiled layout via get_qp)
+                perm = gpu_to_oracle_perm(Nh)
+                stp, Xp, Up, _ = ffi.prologue(kp, cv, Nh, M, x[0], Xin[0], Uin[0], warm=0)
+                q = ffi.build_qp(kp, cv, Nh, M, Xp, Up)
+                gq = g.get_qp(0)
+                Hg = np.zeros_like(q["H"]); Hg[np.ix_(perm, perm)] = gq["H"]
+                assert np.abs(Hg - q["H"]).max() / np.abs(q["H"]).max() < 1e-11
+            x = Xo[:, 1, :].copy()
+        # a few synthetic kites reach the vx >= 2 bound by step 4, where the QP can
+        # be infeasible (oracle and GPU both reject the step, status bit 32)
+        kkt, iters = g.qp_stats()
+        assert np.all((kkt < 1e-8) | ((r["status"] & 32) != 0)), kkt
     finally:
         g.close()
 
