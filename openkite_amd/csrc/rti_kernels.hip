@@ -41,11 +41,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 //   DPP row_newbcast:p    -> lane p of each 16-lane row, to the whole row
 // All of these must be called in wave-uniform control flow.
 // ---------------------------------------------------------------------------
+// 64-bit DPP move.  Every control used here (row_ror, row_newbcast, quad_perm)
+// reads an in-row lane, so the old value is dead: bound_ctrl with no old
+// operand lets the compiler skip the zero-initialisation of the destination,
+// and row_newbcast becomes a single v_mov_b64_dpp.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
+    const long x = __builtin_amdgcn_update_dpp((long)0, __builtin_bit_cast(long, v), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, x);
 }
 // {value of rows [0,0,2,2], value of rows [1,1,3,3]}
 __device__ __forceinline__ void swap16_d(double v, double& ev, double& od) {
