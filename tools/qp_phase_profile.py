@@ -41,6 +41,9 @@ for i, p in enumerate(PHASES):
     per_it = c / (its / ninst) if i in (1, 2, 3, 4, 5, 6) else float("nan")
     print(f"{p:15s} {c:12.0f} cycles/instance  {100 * c / tot:5.1f}%  per-iteration {per_it:10.0f}")
 print(f"{'total':15s} {tot:12.0f}")
+if NH == 20:   # k_qp_tiled Cholesky sub-phases, cycles per instance
+    for i, nm in enumerate(["stage panels", "panels", "trailing + next diagonal"]):
+        print(f"  chol {nm:20s} {v[11 + i] / ninst:12.0f}")
 if NH == 40:   # k_qp_lds sub-phases (wave 0 unless noted), cycles per instance
     for i, nm in enumerate(["load_h+symv", "diag tiles (wave 0)", "trailing (wave 1)", "panel", "msolve sweeps"]):
         print(f"  sub {nm:22s} {v[11 + i] / ninst:12.0f}")
