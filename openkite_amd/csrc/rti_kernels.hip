@@ -484,6 +484,10 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
     __shared__ double Wc[16 * WLDc];
     __shared__ double sG[4];
     __shared__ double sMax[4];
+    // per-variable column scaling D, R diagonal and R ubar of the output
+    // stage (a table: lane-dependent selects over kernel-argument fields
+    // would be lowered to scratch)
+    __shared__ double sScl[16 * NR], sRd[16 * NR], sRu[16 * NR];
     const int b = blockIdx.x;
     const int t = threadIdx.x;
     const int l = t & 63, w = t >> 6;
@@ -495,6 +499,26 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
 
     for (int i = t; i < 16 * WLDc; i += NT) Wc[i] = 0.0;
     if (t < 4) sG[t] = 0.0;
+    {
+        const double iS0 = 1.0 / C.Su[0], iS1 = 1.0 / C.Su[1], iS2 = 1.0 / C.Su[2], iS3 = 1.0 / C.Su[3];
+        const double R0 = C.Rdiag[0], R1 = C.Rdiag[1], R2 = C.Rdiag[2], R3 = C.Rdiag[3];
+        for (int i = t; i < 16 * NR; i += NT) {
+            double sc = 0.0, rd = 0.0, ub = 0.0;
+            if (i < 3 * N) {
+                const int c = i % 3;
+                sc = c == 0 ? iS0 : (c == 1 ? iS1 : iS2);
+                rd = c == 0 ? R0 : (c == 1 ? R1 : R2);
+                ub = Ub[(i / 3) * NU + c];
+            } else if (i < 4 * N) {
+                sc = iS3; rd = R3; ub = Ub[(i - 3 * N) * NU + 3];
+            } else if (i == 4 * N) {
+                sc = 1.0 / C.Sx13;
+            } else if (i == 4 * N + 1) {
+                sc = 1.0 / C.Sx14;
+            }
+            sScl[i] = sc; sRd[i] = rd; sRu[i] = rd * ub;
+        }
+    }
 
     const bool kite_lane = t < 3 * N;
     const bool aff_lane = (t == 3 * N);
@@ -637,7 +661,6 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
     const int na = 4 * N;
     const int ntile = (N / 4) * (N / 4 + 1) / 2;       // tiled: lower tiles of H_aa (N % 4 == 0)
     double lmax = 0.0;
-    const ColConst K = col_const(C);
     auto put = [&](int I, int J, double4v a4) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -646,8 +669,8 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
             const double a = a4[r];
             if (gi < n && gj < n) {
                 double hv = a;
-                if (gi == gj) hv += col_rdiag(K, gi);
-                hv *= col_scale(K, gi) * col_scale(K, gj);
+                if (gi == gj) hv += sRd[gi];
+                hv *= sScl[gi] * sScl[gj];
                 if (tiled) {
                     if (gi < na) Htl[((size_t)b * ntile + I * (I + 1) / 2 + J) * 256 + r * 64 + l] = hv;
                     else if (gj < na) Hab[((size_t)b * na + gj) * 2 + (gi - na)] = hv;
@@ -661,7 +684,7 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
                 }
                 lmax = fmax(lmax, fabs(hv));
             } else if (gi == n && gj < n) {
-                hs[(size_t)b * n + gj] = (a + col_rdiag(K, gj) * col_ubar(C, Ub, gj)) * col_scale(K, gj);
+                hs[(size_t)b * n + gj] = (a + sRu[gj]) * sScl[gj];
             }
         }
     };
@@ -709,10 +732,19 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     const bool accept = kkt < QP_STEP_ACCEPT;
     // physical step dw = D w_s into vec
     if constexpr (WAVE) wave_sync(); else __syncthreads();
+    {
+        // column scale by value selects (a lane-dependent index into the
+        // kernel-argument struct would copy it to scratch)
+        const double iS0 = 1.0 / C.Su[0], iS1 = 1.0 / C.Su[1], iS2 = 1.0 / C.Su[2], iS3 = 1.0 / C.Su[3];
+        const double iX13 = 1.0 / C.Sx13, iX14 = 1.0 / C.Sx14;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        const int i = l + 64 * s;
-        if (i < n) vec[i] = accept ? w[s] * col_scale(C, i) : 0.0;
+        for (int s = 0; s < NS; ++s) {
+            const int i = l + 64 * s;
+            const int c = i % 3;
+            const double sc = i < 3 * N ? (c == 0 ? iS0 : (c == 1 ? iS1 : iS2))
+                                        : (i < 4 * N ? iS3 : (i == 4 * N ? iX13 : iX14));
+            if (i < n) vec[i] = accept ? w[s] * sc : 0.0;
+        }
     }
     if constexpr (WAVE) wave_sync(); else __syncthreads();
     const double dth0 = vec[4 * N], dthd0 = vec[4 * N + 1];
@@ -734,21 +766,37 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     }
     // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row)
     {
+        // row l of [A_k | B_k], d_k and x_{k+1} are prefetched one interval
+        // ahead (the recursion itself is a chain of N dependent steps)
         double dx = 0.0;
         const double* ABb = AB + (size_t)b * N * NK * 16;
         const double* DEFb = DEF + (size_t)b * N * NK;
+        const int lr = l < NK ? l : NK - 1;
+        double ar[16], dk = 0.0, xk1 = 0.0;
+        auto fetch = [&](int k) __attribute__((always_inline)) {
+            const double* p = ABb + ((size_t)k * NK + lr) * 16;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) ar[j] = p[j];
+            dk = DEFb[(size_t)k * NK + lr];
+            xk1 = Xb[(k + 1) * NX + lr];
+        };
+        if (N > 0) fetch(0);
         for (int k = 0; k < N; ++k) {
+            double a[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) a[j] = ar[j];
+            const double d = dk, xo = xk1;
+            if (k + 1 < N) fetch(k + 1);
             if constexpr (WAVE) wave_sync(); else __syncthreads();
             if (l < NK) col[l] = dx;
             if constexpr (WAVE) wave_sync(); else __syncthreads();
-            if (l < NK) {
-                const double* ar = ABb + ((size_t)k * NK + l) * 16;
-                double t = DEFb[(size_t)k * NK + l];
-                for (int j = 0; j < NK; ++j) t = fma(ar[j], col[j], t);
-                for (int c = 0; c < 3; ++c) t = fma(ar[NK + c], vec[3 * k + c], t);
-                dx = t;
-                Xb[(k + 1) * NX + l] += dx;
-            }
+            double t = d;
+#pragma unroll
+            for (int j = 0; j < NK; ++j) t = fma(a[j], col[j], t);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) t = fma(a[NK + c], vec[3 * k + c], t);
+            dx = t;
+            if (l < NK) Xb[(k + 1) * NX + l] = xo + dx;
         }
     }
     if constexpr (WAVE) wave_sync(); else __syncthreads();
