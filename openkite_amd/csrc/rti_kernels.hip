@@ -469,8 +469,22 @@ __device__ __forceinline__ void wave_put(int w, const double4v* acc, F& put) {
     else if constexpr (W + 1 < CondenseGeom<NR>::NW) wave_put<NR, W + 1>(w, acc, put);
 }
 
+// Optional phase profile of k_condense (-DKITE_QP_PROF, tools only): shader
+// clock cycles of wave 0 per phase, summed over instances into g_cd_prof.
+#ifdef KITE_QP_PROF
+__device__ unsigned long long g_cd_prof[8];
+#define CD_MARK(ph)                                                                  \
+    do {                                                                             \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+        cd_acc[ph] += t_ - cd_last;                                                  \
+        cd_last = t_;                                                                \
+    } while (0)
+#else
+#define CD_MARK(ph) do { } while (0)
+#endif
+
 template <int NR>
-__global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst C, int B, const double* __restrict__ X,
+__global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_waves_per_eu(NR <= 7 ? 2 : 1))) void k_condense(RtiConst C, int B, const double* __restrict__ X,
                                                   const double* __restrict__ U, const double* __restrict__ AB,
                                                   const double* __restrict__ DEF, double* __restrict__ Hs,
                                                   double* __restrict__ hs, double* __restrict__ Cr,
@@ -480,14 +494,23 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
     using Gm = CondenseGeom<NR>;
     constexpr int WLDc = Gm::WLD;
     constexpr int NT = 64 * Gm::NW;
-    __shared__ double sA[NK * 16 + NK + 3];
+    constexpr int NMAX = (16 * NR - 3) / 4;          // largest horizon with n + 1 <= 16 NR
+    constexpr int SAL = 16 * 16 + NK + 3;
+    __shared__ double sA[2][SAL];                    // [A_k | B_k] by columns (col j: 16 j + i), then d_k;
+                                                     // double-buffered by node parity
     __shared__ double Wc[16 * WLDc];
-    __shared__ double sG[4];
+    __shared__ double sG[2][4];                      // affine column rows 0, 6..8, by node parity
+    __shared__ double sX[(NMAX + 1) * NX];           // linearisation trajectory
+    __shared__ double sPth[NMAX + 1][6];             // P(theta_k), dP/dtheta(theta_k)
     __shared__ double sMax[4];
     // per-variable column scaling D, R diagonal and R ubar of the output
     // stage (a table: lane-dependent selects over kernel-argument fields
     // would be lowered to scratch)
     __shared__ double sScl[16 * NR], sRd[16 * NR], sRu[16 * NR];
+#ifdef KITE_QP_PROF
+    unsigned long long cd_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long cd_last = __builtin_amdgcn_s_memtime();
+#endif
     const int b = blockIdx.x;
     const int t = threadIdx.x;
     const int l = t & 63, w = t >> 6;
@@ -498,7 +521,16 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
     const double* DEFb = DEF + (size_t)b * N * NK;
 
     for (int i = t; i < 16 * WLDc; i += NT) Wc[i] = 0.0;
-    if (t < 4) sG[t] = 0.0;
+    if (t < 8) sG[t >> 2][t & 3] = 0.0;
+    // the trajectory and the path at every node up front (lane per node): the
+    // node loop below is a dependent chain and reads both from LDS only
+    for (int i = t; i < (N + 1) * NX; i += NT) sX[i] = Xb[i];
+    if (t <= N) {
+        double Pp[3], dP[3];
+        path_eval(C, Xb[t * NX + 13], Pp, dP);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { sPth[t][a] = Pp[a]; sPth[t][3 + a] = dP[a]; }
+    }
     {
         const double iS0 = 1.0 / C.Su[0], iS1 = 1.0 / C.Su[1], iS2 = 1.0 / C.Su[2], iS3 = 1.0 / C.Su[3];
         const double R0 = C.Rdiag[0], R1 = C.Rdiag[1], R2 = C.Rdiag[2], R3 = C.Rdiag[3];
@@ -532,32 +564,56 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
 #pragma unroll
     for (int q = 0; q < Gm::ACC; ++q) acc[q] = double4v{0.0, 0.0, 0.0, 0.0};
 
-    // software prefetch of interval data (221 doubles -> <= 4 per thread)
+    // software prefetch of the interval data (221 doubles -> <= 2 per thread),
+    // PD intervals ahead in a register ring: the node loop is a dependent
+    // chain, so one interval of look-ahead would expose the global latency
     constexpr int NPF = (NK * 16 + NK + NT - 1) / NT;
-    double pf[NPF];
-#define KITE_LOAD_INTERVAL(k)                                                              \
-    _Pragma("unroll") for (int q = 0; q < NPF; ++q) {                                      \
-        const int e = t + NT * q;                                                          \
-        double val = 0.0;                                                                  \
-        if (e < NK * 16) val = ABb[(size_t)(k) * NK * 16 + e];                             \
-        else if (e < NK * 16 + NK) val = DEFb[(size_t)(k) * NK + (e - NK * 16)];           \
-        pf[q] = val;                                                                       \
-    }
-    if (N > 0) { KITE_LOAD_INTERVAL(0) }
+    constexpr int PD = 2;
+    double pf[PD][NPF];
+    auto load_iv = [&](int k, double* dst) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < NPF; ++q) {
+            const int e = t + NT * q;
+            double val = 0.0;
+            if (e < NK * 16) val = ABb[(size_t)k * NK * 16 + e];
+            else if (e < NK * 16 + NK) val = DEFb[(size_t)k * NK + (e - NK * 16)];
+            dst[q] = val;
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+        if (s < N) load_iv(s, pf[s]);
     __syncthreads();
 
     // residual row weights in registers: stage sqrt(dt Q) Sr, Mayer sqrt(Q) Sr
     double wpD[3], wpT[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) { wpD[a] = C.sqQ_dt[a] * C.Sr[a]; wpT[a] = C.sqQ_T[a] * C.Sr[a]; }
-    for (int k = 0; k <= N; ++k) {
+    // Node loop, one barrier per node: sA and sG are double-buffered by node
+    // parity, so the barrier that publishes interval k also orders the affine
+    // values of node k (written after the previous barrier) and the previous
+    // chunk fold before this node's W rows overwrite Wc.
+    CD_MARK(0);
+    auto node = [&](int k, double* pfs) __attribute__((always_inline)) {
         const bool last = (k == N);
-        const double* xk = Xb + k * NX;
-        const double th = xk[13], thd = xk[14];
-        double Pp[3], dP[3];
-        path_eval(C, th, Pp, dP);
-        const double g0 = sG[0];
-        const double gr[3] = {sG[1], sG[2], sG[3]};
+        const int par = k & 1;
+        if (!last) {
+#pragma unroll
+            for (int q = 0; q < NPF; ++q) {
+                const int e = t + NT * q;
+                if (e < NK * 16) sA[par][(e & 15) * 16 + (e >> 4)] = pfs[q];      // transpose: column-major
+                else if (e < NK * 16 + NK) sA[par][16 * 16 + (e - NK * 16)] = pfs[q];
+            }
+        }
+        __syncthreads();
+        CD_MARK(1);
+        if (k + PD < N) load_iv(k + PD, pfs);
+        const double* xk = sX + k * NX;
+        const double thd = xk[14];
+        const double Pp[3] = {sPth[k][0], sPth[k][1], sPth[k][2]};
+        const double dP[3] = {sPth[k][3], sPth[k][4], sPth[k][5]};
+        const double g0 = sG[par ^ 1][0];
+        const double gr[3] = {sG[par ^ 1][1], sG[par ^ 1][2], sG[par ^ 1][3]};
         double wp[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) wp[a] = last ? wpT[a] : wpD[a];
@@ -608,9 +664,47 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
             for (int r = row0 + 4; r < 16; ++r)
                 for (int cidx = t; cidx <= n; cidx += NT) Wc[r * WLDc + cidx] = 0.0;
         }
+        CD_MARK(2);
+        if (!last) {
+            // propagate G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
+            const double* sa = sA[par];
+            if ((kite_lane && k >= kb) || aff_lane) {
+                double nv[NK];
+                if (kite_lane && k == kb) {
+#pragma unroll
+                    for (int i = 0; i < NK; ++i) nv[i] = sa[(NK + cc) * 16 + i];
+                } else {
+                    // column-oriented: 13 independent accumulator chains, the
+                    // next column's loads in flight under this column's FMAs
+                    const double am = aff_lane ? 1.0 : 0.0;
+#pragma unroll
+                    for (int i = 0; i < NK; ++i) nv[i] = am * sa[16 * 16 + i];
+                    double ac[NK], an[NK];
+#pragma unroll
+                    for (int i = 0; i < NK; ++i) ac[i] = sa[i];
+#pragma unroll
+                    for (int j = 0; j < NK; ++j) {
+                        if (j + 1 < NK) {
+#pragma unroll
+                            for (int i = 0; i < NK; ++i) an[i] = sa[(j + 1) * 16 + i];
+                        }
+#pragma unroll
+                        for (int i = 0; i < NK; ++i) nv[i] = fma(ac[i], v[j], nv[i]);
+                        asm volatile("" ::: "memory");   // at most two columns of A_k in registers
+#pragma unroll
+                        for (int i = 0; i < NK; ++i) ac[i] = an[i];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NK; ++i) v[i] = nv[i];
+            }
+            if (aff_lane) { sG[par][0] = v[0]; sG[par][1] = v[6]; sG[par][2] = v[7]; sG[par][3] = v[8]; }
+        }
+        CD_MARK(3);
         if ((k & 3) == 3 || last) {
             __syncthreads();
             // fold the chunk: every wave into the tiles of its own tile rows
+            // (the next node's barrier orders these reads before Wc is rewritten)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 double fr[NR];
@@ -618,40 +712,16 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
                 for (int I = 0; I < NR; ++I) fr[I] = Wc[(4 * s + (l >> 4)) * WLDc + 16 * I + (l & 15)];
                 wave_fold<NR, 0>(w, acc, fr);
             }
-            __syncthreads();
+            CD_MARK(4);
         }
-        if (last) break;
-
-        // propagate G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
-#pragma unroll
-        for (int q = 0; q < NPF; ++q) {
-            const int e = t + NT * q;
-            if (e < NK * 16 + NK) sA[e] = pf[q];
-        }
-        __syncthreads();
-        if (k + 1 < N) { KITE_LOAD_INTERVAL(k + 1) }
-        if ((kite_lane && k >= kb) || aff_lane) {
-            double nv[NK];
-            if (kite_lane && k == kb) {
-#pragma unroll
-                for (int i = 0; i < NK; ++i) nv[i] = sA[i * 16 + NK + cc];
-            } else {
-#pragma unroll
-                for (int i = 0; i < NK; ++i) {
-                    double tt = aff_lane ? sA[NK * 16 + i] : 0.0;
-#pragma unroll
-                    for (int j = 0; j < NK; ++j) tt = fma(sA[i * 16 + j], v[j], tt);
-                    nv[i] = tt;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < NK; ++i) v[i] = nv[i];
-        }
-        __syncthreads();
-        if (aff_lane) { sG[0] = v[0]; sG[1] = v[6]; sG[2] = v[7]; sG[3] = v[8]; }
-        __syncthreads();
+    };
+#pragma unroll 1
+    for (int k0 = 0; k0 <= N; k0 += PD) {
+        node(k0, pf[0]);
+        if (k0 + 1 > N) break;
+        node(k0 + 1, pf[1]);
     }
-#undef KITE_LOAD_INTERVAL
+    __syncthreads();
 
     // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar).
     // tiled != 0 (k_qp_tiled N = 20, k_qp_lds N = 40): the control block H_aa (na = 4N = 16*NT)
@@ -697,7 +767,24 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) void k_condense(RtiConst
         for (int i = 1; i < Gm::NW; ++i) m = fmax(m, sMax[i]);
         hmax[b] = m;
     }
+#ifdef KITE_QP_PROF
+    CD_MARK(5);
+    if (t == 0) {
+        for (int i = 0; i < 6; ++i) atomicAdd(&g_cd_prof[i], cd_acc[i]);
+        atomicAdd(&g_cd_prof[7], 1ull);
+    }
+#endif
 }
+
+#ifdef KITE_QP_PROF
+// tools only: read and clear the condensing phase profile (8 x uint64)
+extern "C" int kite_debug_cd_profile(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cd_prof), sizeof(g_cd_prof)) != hipSuccess) return -1;
+    const unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_cd_prof), z, sizeof(z)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // k_qp: one wavefront per instance.  Mehrotra predictor-corrector primal-dual

@@ -29,9 +29,17 @@ x = x0_batch(B)
 for step in range(4):
     r = g.step(x)
     x = r["traj"][:, 1, :].copy()
+L.kite_debug_cd_profile.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+cbuf = (ctypes.c_ulonglong * 8)()
 L.kite_debug_qp_profile(buf)          # clear warm-up
+L.kite_debug_cd_profile(cbuf)
 r = g.step(x)
 L.kite_debug_qp_profile(buf)
+L.kite_debug_cd_profile(cbuf)
+cv = np.array(cbuf[:8], dtype=np.float64)
+print("k_condense (wave 0), cycles per instance:")
+for i, nm in enumerate(["init", "node barrier", "W rows", "propagate", "fold", "output"]):
+    print(f"  {nm:15s} {cv[i] / max(cv[7], 1):12.0f}")
 v = np.array(buf[:16], dtype=np.float64)
 ninst, its = v[10], v[9]
 print(f"B={B} N={NH} instances={ninst:.0f} mean iterations={its / ninst:.2f}")
