@@ -851,10 +851,12 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         const int k = e / NU, c = e % NU;
         Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
     }
-    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row)
+    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row).
+    // The recursion is a chain of N dependent steps: dx_k is broadcast from
+    // lanes 0..12 by v_readlane (no LDS round trip, no barrier), the row dot
+    // product runs as four partial sums, and row l of [A_k | B_k], d_k and
+    // x_{k+1} are prefetched one interval ahead.
     {
-        // row l of [A_k | B_k], d_k and x_{k+1} are prefetched one interval
-        // ahead (the recursion itself is a chain of N dependent steps)
         double dx = 0.0;
         const double* ABb = AB + (size_t)b * N * NK * 16;
         const double* DEFb = DEF + (size_t)b * N * NK;
@@ -874,15 +876,16 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
             for (int j = 0; j < 16; ++j) a[j] = ar[j];
             const double d = dk, xo = xk1;
             if (k + 1 < N) fetch(k + 1);
-            if constexpr (WAVE) wave_sync(); else __syncthreads();
-            if (l < NK) col[l] = dx;
-            if constexpr (WAVE) wave_sync(); else __syncthreads();
-            double t = d;
+            double t0 = fma(a[NK], vec[3 * k], d), t1 = a[NK + 1] * vec[3 * k + 1];
+            double t2 = a[NK + 2] * vec[3 * k + 2], t3 = 0.0;
 #pragma unroll
-            for (int j = 0; j < NK; ++j) t = fma(a[j], col[j], t);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) t = fma(a[NK + c], vec[3 * k + c], t);
-            dx = t;
+            for (int j = 0; j < NK; j += 4) {
+                t0 = fma(a[j], readlane_d(dx, j), t0);
+                if (j + 1 < NK) t1 = fma(a[j + 1], readlane_d(dx, j + 1), t1);
+                if (j + 2 < NK) t2 = fma(a[j + 2], readlane_d(dx, j + 2), t2);
+                if (j + 3 < NK) t3 = fma(a[j + 3], readlane_d(dx, j + 3), t3);
+            }
+            dx = (t0 + t1) + (t2 + t3);
             if (l < NK) Xb[(k + 1) * NX + l] = xo + dx;
         }
     }
