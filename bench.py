@@ -202,6 +202,7 @@ def main():
     elapsed = time.perf_counter() - t0
     nrec, ksum = ctx.timing_read()
     kkt, iters = ctx.qp_stats()
+    it_sum = ctx.qp_iteration_sum()
     status = d_status.cpu().numpy()
 
     elapsed_max = max_over_ranks(elapsed, dev)
@@ -209,7 +210,9 @@ def main():
     value = total_rti / elapsed_max
 
     if rank == 0:
-        mean_it = float(np.mean(iters))
+        # mean over every instance of every timed step (device-side running
+        # sums restarted by timing_start), not just the last step
+        mean_it = it_sum / float(B * args.steps)
         fl = flops.rti(N, args.substeps, mean_it)
         kernels = ["prologue", "rk4_sens", "condense", "qp"]
         avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels}

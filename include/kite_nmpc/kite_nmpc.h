@@ -263,6 +263,10 @@ int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n);
 /* QP statistics of the last step: final residual and interior-point
  * iterations per instance (host pointers, B each; either may be NULL).    */
 int kite_nmpc_qp_stats(kite_nmpc_ctx* ctx, double* kkt, int32_t* iters);
+/* Interior-point iterations summed over all instances and all steps since
+ * the last kite_nmpc_timing_start (or since create): the measurement hook
+ * behind bench.py's FLOP count (no reference counterpart).                */
+int kite_nmpc_qp_iteration_sum(kite_nmpc_ctx* ctx, int64_t* sum);
 /* Condensed QP of one instance from the last step (scaled variables, GPU
  * column order: [T,dE,dR]_k (3N) | Uv_k (N) | theta0 | thetadot0).
  * H n x n, h n, C N x n, cl/cu N (+-INF = absent), n = 4N+2.               */

@@ -374,9 +374,9 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         (void)hipMemset(*a.p, 0, a.count * sizeof(double));
     }
     if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&ctx->iters, B * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
+        hipMalloc(&ctx->iters, 2 * B * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
     (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
-    (void)hipMemset(ctx->iters, 0, B * sizeof(int32_t));
+    (void)hipMemset(ctx->iters, 0, 2 * B * sizeof(int32_t));   // [0, B): last step, [B, 2B): running sum
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
         free_ctx(ctx); delete ctx; return KITE_EHIP;
     }
@@ -785,6 +785,8 @@ int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
     }
     ctx->ring_cap = max_steps;
     ctx->ring_used = 0;
+    // restart the per-instance QP iteration sums (second half of ctx->iters)
+    HIP_TRY(hipMemsetAsync(ctx->iters + ctx->B, 0, (size_t)ctx->B * sizeof(int32_t), ctx->stream));
     return KITE_OK;
 }
 
@@ -818,6 +820,19 @@ int kite_nmpc_qp_stats(kite_nmpc_ctx* ctx, double* kkt, int32_t* iters) {
     if (kkt) HIP_TRY(hipMemcpyAsync(kkt, ctx->kkt, B * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     if (iters) HIP_TRY(hipMemcpyAsync(iters, ctx->iters, B * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return KITE_OK;
+}
+
+int kite_nmpc_qp_iteration_sum(kite_nmpc_ctx* ctx, int64_t* sum) {
+    if (!ctx || !sum) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<int32_t> acc(ctx->B);
+    HIP_TRY(hipMemcpyAsync(acc.data(), ctx->iters + ctx->B, acc.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int64_t t = 0;
+    for (int32_t v : acc) t += v;
+    *sum = t;
     return KITE_OK;
 }
 

@@ -811,6 +811,7 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
                              double* __restrict__ Xb, double* __restrict__ Ub, double* __restrict__ u0_out,
                              double* __restrict__ diag, int32_t* __restrict__ status,
                              double* __restrict__ kkt_out, int32_t* __restrict__ iters_out,
+                             int32_t* __restrict__ iters_acc,
                              double* vec, double* col) {
     const int N = C.N, n = C.n;
     // ---- expansion and trajectory update ------------------------------------
@@ -940,6 +941,7 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         status[b] = st;
         if (kkt_out) kkt_out[b] = kkt;
         if (iters_out) iters_out[b] = iters;
+        if (iters_acc) iters_acc[b] += iters;          // running sum since kite_nmpc_timing_start
         for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
     }
 }
@@ -1336,7 +1338,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     residuals();
     const double kkt = resid;
 
-    rti_epilogue<NS>(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out, vec, col);
+    rti_epilogue<NS>(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out,
+                     iters_out ? iters_out + B : nullptr, vec, col);
 }
 
 // ---------------------------------------------------------------------------

@@ -129,6 +129,7 @@ _SIGNATURES = {
     "kite_nmpc_timing_start": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
+    "kite_nmpc_qp_iteration_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "kite_ekf_default_covariances": (None, [_DP, _DP, _DP]),
     "kite_colloc_default_config": (None, [ctypes.c_void_p]),
     "kite_nmpc_colloc_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP]),
@@ -309,6 +310,12 @@ class BatchNMPC:
         kkt = np.zeros(self.batch); it = np.zeros(self.batch, dtype=np.int32)
         _check(lib().kite_nmpc_qp_stats(self._h, _p(kkt), it.ctypes.data_as(_IP)), "qp_stats")
         return kkt, it
+
+    def qp_iteration_sum(self) -> int:
+        """QP iterations summed over instances and steps since timing_start."""
+        v = ctypes.c_int64(0)
+        _check(lib().kite_nmpc_qp_iteration_sum(self._h, ctypes.byref(v)), "qp_iteration_sum")
+        return int(v.value)
 
     def get_qp(self, instance: int):
         n = 4 * self.N + 2

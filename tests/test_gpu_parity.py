@@ -293,6 +293,30 @@ def test_full_batch_properties():
 
 
 @pytest.mark.parametrize("qp_kernel", [1, 2])
+def test_qp_iteration_sum_matches_per_step_counts(qp_kernel):
+    """kite_nmpc_qp_iteration_sum (bench.py's FLOP count) = the per-step
+    iteration counts of kite_nmpc_qp_stats summed over steps and instances,
+    restarted by kite_nmpc_timing_start; both QP kernels."""
+    B = 64
+    cfg = ok.default_config(qp_kernel=qp_kernel)
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    try:
+        x0 = x0_batch(B)
+        r = g.step(x0)                       # before timing_start: not counted
+        g.timing_start(8)
+        total = 0
+        x0 = r["traj"][:, 1, :].copy()
+        for _ in range(3):
+            r = g.step(x0)
+            total += int(g.qp_stats()[1].sum())
+            x0 = r["traj"][:, 1, :].copy()
+        assert g.qp_iteration_sum() == total
+        assert total >= 3 * B                # every QP iterated at least once
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("qp_kernel", [1, 2])
 def test_qp_kernels_vs_oracle(kp, cfgv, qp_kernel):
     """Both QP kernels (1 = wave-scalar, 2 = MFMA-tiled) against the oracle."""
     B = 16
