@@ -952,6 +952,14 @@ constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.99
 // freezing that direction for the step; NaN stays NaN.
 constexpr double KITE_PIV_BIG = 1e128;
 __device__ __forceinline__ double piv_fix(double s) { return s <= 0.0 ? KITE_PIV_BIG : s; }
+// 1/sqrt(p): v_rsq_f64 estimate y (~2^-23) + one third-order correction
+// y (1 + e/2 + 3e^2/8), e = 1 - p y^2 (~1 ulp; the IEEE sqrt + division
+// sequence is ~20 instructions)
+__device__ __forceinline__ double fast_rsq(double p) {
+    const double y = __builtin_amdgcn_rsq(p);
+    const double e = fma(-p, y * y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
+}
 
 __device__ __forceinline__ int pk(int i, int c) { return (i * (i + 1)) / 2 + c; }
 
