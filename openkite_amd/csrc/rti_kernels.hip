@@ -27,6 +27,12 @@ namespace kite {
 // ---------------------------------------------------------------------------
 // small device helpers
 // ---------------------------------------------------------------------------
+// a wave-uniform double moved to SGPRs (frees two VGPRs for as long as it lives)
+__device__ __forceinline__ double uniform_d(double v) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+    const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     int lo = __double2loint(v), hi = __double2hiint(v);
     lo = __builtin_amdgcn_readlane(lo, lane);
