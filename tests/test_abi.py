@@ -105,6 +105,10 @@ def test_create_fails_loudly_without_device_and_validates():
     with pytest.raises(ok.KiteNmpcError) as e:
         ok.BatchNMPC(p, bad, 4)
     assert e.value.code == nmpc.KITE_EINVAL
+    for b in (0, -3):                      # empty / negative batch: rejected before any device work
+        with pytest.raises(ok.KiteNmpcError) as e:
+            ok.BatchNMPC(p, ok.default_config(), b)
+        assert e.value.code == nmpc.KITE_EINVAL
     bad = ok.default_config(N=21)          # beyond the fused kernels' horizon
     with pytest.raises(ok.KiteNmpcError):
         ok.BatchNMPC(p, bad, 4)

@@ -162,6 +162,26 @@ def test_rti_steps_vs_oracle(kp, cfgv):
     print(f"RTI GPU vs oracle worst relative error over 6 steps: {worst:.3e}")
 
 
+@pytest.mark.parametrize("B", [1, 37])
+def test_ragged_batch_vs_oracle(kp, cfgv, B):
+    """Batches that fill no block evenly (rk4_sens: 8 kites per block,
+    prologue: 64 per block) and the single-kite case, 3 closed-loop steps."""
+    x = x0_batch(B, offset=3000)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    try:
+        for step in range(3):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            assert np.all(np.isfinite(r["traj"]))
+            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+            assert e < RTI_TOL, (B, step, e)
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+
+
 def test_delay_compensation_vs_oracle(kp):
     """Fused transport-delay compensation (config.delay = 0.1 s, the node's
     default, nmpf_node.cpp:74): 5 closed-loop steps of 16 kites vs the oracle."""
