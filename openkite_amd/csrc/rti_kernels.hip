@@ -530,7 +530,20 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
     if (t < 8) sG[t >> 2][t & 3] = 0.0;
     // the trajectory and the path at every node up front (lane per node): the
     // node loop below is a dependent chain and reads both from LDS only
-    for (int i = t; i < (N + 1) * NX; i += NT) sX[i] = Xb[i];
+    {
+        constexpr int NXL = ((NMAX + 1) * NX + NT - 1) / NT;    // loads per thread, all in flight
+        double xv[NXL];
+#pragma unroll
+        for (int q = 0; q < NXL; ++q) {
+            const int i = t + NT * q;
+            xv[q] = i < (N + 1) * NX ? Xb[i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NXL; ++q) {
+            const int i = t + NT * q;
+            if (i < (N + 1) * NX) sX[i] = xv[q];
+        }
+    }
     if (t <= N) {
         double Pp[3], dP[3];
         path_eval(C, Xb[t * NX + 13], Pp, dP);
