@@ -875,27 +875,29 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
     // The recursion is a chain of N dependent steps: dx_k is broadcast from
     // lanes 0..12 by v_readlane (no LDS round trip, no barrier), the row dot
     // product runs as four partial sums, and row l of [A_k | B_k], d_k and
-    // x_{k+1} are prefetched one interval ahead.
+    // x_{k+1} come from a register ring PD intervals ahead (one interval of
+    // look-ahead would expose a global-memory latency per interval; the QP's
+    // registers are free by now).
     {
+        constexpr int PD = 4;
         double dx = 0.0;
         const double* ABb = AB + (size_t)b * N * NK * 16;
         const double* DEFb = DEF + (size_t)b * N * NK;
         const int lr = l < NK ? l : NK - 1;
-        double ar[16], dk = 0.0, xk1 = 0.0;
-        auto fetch = [&](int k) __attribute__((always_inline)) {
+        double ar[PD][16], dk[PD], xk1[PD];
+        auto fetch = [&](int k, double* a, double& d, double& x) __attribute__((always_inline)) {
             const double* p = ABb + ((size_t)k * NK + lr) * 16;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) ar[j] = p[j];
-            dk = DEFb[(size_t)k * NK + lr];
-            xk1 = Xb[(k + 1) * NX + lr];
+            for (int j = 0; j < 16; ++j) a[j] = p[j];
+            d = DEFb[(size_t)k * NK + lr];
+            x = Xb[(k + 1) * NX + lr];
         };
-        if (N > 0) fetch(0);
-        for (int k = 0; k < N; ++k) {
+        auto interval = [&](int k, double* ring, double& dring, double& xring) __attribute__((always_inline)) {
             double a[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) a[j] = ar[j];
-            const double d = dk, xo = xk1;
-            if (k + 1 < N) fetch(k + 1);
+            for (int j = 0; j < 16; ++j) a[j] = ring[j];
+            const double d = dring, xo = xring;
+            if (k + PD < N) fetch(k + PD, ring, dring, xring);
             double t0 = fma(a[NK], vec[3 * k], d), t1 = a[NK + 1] * vec[3 * k + 1];
             double t2 = a[NK + 2] * vec[3 * k + 2], t3 = 0.0;
 #pragma unroll
@@ -907,6 +909,18 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
             }
             dx = (t0 + t1) + (t2 + t3);
             if (l < NK) Xb[(k + 1) * NX + l] = xo + dx;
+        };
+#pragma unroll
+        for (int q = 0; q < PD; ++q)
+            if (q < N) fetch(q, ar[q], dk[q], xk1[q]);
+        for (int k0 = 0; k0 < N; k0 += PD) {
+            interval(k0, ar[0], dk[0], xk1[0]);
+            if (k0 + 1 >= N) break;
+            interval(k0 + 1, ar[1], dk[1], xk1[1]);
+            if (k0 + 2 >= N) break;
+            interval(k0 + 2, ar[2], dk[2], xk1[2]);
+            if (k0 + 3 >= N) break;
+            interval(k0 + 3, ar[3], dk[3], xk1[3]);
         }
     }
     if constexpr (WAVE) wave_sync(); else __syncthreads();
