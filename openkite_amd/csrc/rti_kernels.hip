@@ -183,73 +183,117 @@ __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* 
 }
 
 // ---------------------------------------------------------------------------
-// k_prologue: lane per instance.  theta wrap (kiteNMPF.cpp:209-221), min
-// speed clamp (nmpf_node.cpp:241-243), warm-start shift or cold start
+// k_prologue: one wavefront per instance.  theta wrap (kiteNMPF.cpp:209-221),
+// min speed clamp (nmpf_node.cpp:241-243), warm-start shift or cold start
 // (controls at the bound midpoint kiteNMPF.cpp:192-196, states by forward
-// simulation), x_0 pinned, theta/thetadot re-simulated exactly.
+// simulation), x_0 pinned, theta/thetadot re-simulated exactly.  The per-kite
+// scalar logic runs on lane 0; the warm-start shift (the bulk of the bytes)
+// is a coalesced copy by the whole wave.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64, 2) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
+__global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
                                                  const double* __restrict__ x0in,
                                                  double* __restrict__ X, double* __restrict__ U,
                                                  int32_t* __restrict__ status) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ double sx0[NX];
+    __shared__ double sUv[KITE_NMAX];
+    __shared__ int sWarm;
+    const int b = blockIdx.x;
+    const int l = threadIdx.x;
     if (b >= B) return;
     const int N = C.N;
     double* Xb = X + (size_t)b * (N + 1) * NX;
     double* Ub = U + (size_t)b * N * NU;
-    double x0[NX];
-    for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
     int32_t st = 0;
-    if (warm) {
-        // a non-finite plan (a NaN iterate of a previous step) cannot seed a
-        // warm start: restart this kite cold, theta re-initialised by the
-        // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236).
-        // The previous epilogue flagged it (KITE_ST_NAN: non-finite X or U);
-        // kite_nmpc_set_solution flags injected plans the same way.
-        if (status[b] & 1) {
-            warm = 0;
-            st |= 64;
-            x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
-            x0[14] = 0.0;
+    if (l == 0) {
+        double x0[NX];
+        for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
+        int wm = warm;
+        if (wm) {
+            // a non-finite plan (a NaN iterate of a previous step) cannot seed a
+            // warm start: restart this kite cold, theta re-initialised by the
+            // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236).
+            // The previous epilogue flagged it (KITE_ST_NAN: non-finite X or U);
+            // kite_nmpc_set_solution flags injected plans the same way.
+            if (status[b] & 1) {
+                wm = 0;
+                st |= 64;
+                x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
+                x0[14] = 0.0;
+            }
         }
+        if (wm && C.delay > 0.0) {
+            // transport-delay compensation (nmpf_node.cpp:206-221): predict the
+            // measured kite state over `delay` under the previous u(t0); theta,
+            // thetadot from the previous trajectory at t0 + delay
+            const double up[NU] = {Ub[0], Ub[1], Ub[2], 0.0};
+            double xp[NX];
+            rk4_primal(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp);
+            for (int i = 0; i < 13; ++i) x0[i] = xp[i];
+            x0[13] = Xb[C.delay_node * NX + 13];
+            x0[14] = Xb[C.delay_node * NX + 14];
+        }
+        const double twopi = 2.0 * M_PI;
+        if (x0[13] > twopi) { x0[13] -= twopi; st |= 16; }
+        else if (x0[13] < -twopi) { x0[13] += twopi; st |= 16; }
+        if (x0[0] < C.min_speed) { x0[0] = C.min_speed; st |= 4; }
+        if (!wm) {
+            for (int k = 0; k < N; ++k)
+                for (int j = 0; j < NU; ++j) Ub[k * NU + j] = 0.5 * (C.lbu[j] + C.ubu[j]);
+            for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
+            for (int k = 0; k < N; ++k) rk4_primal(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX]);
+            for (int k = 0; k < N; ++k) sUv[k] = Ub[k * NU + 3];
+        } else if (!C.shift) {
+            for (int k = 0; k < N; ++k) sUv[k] = Ub[k * NU + 3];
+        }
+        for (int i = 0; i < NX; ++i) sx0[i] = x0[i];
+        sWarm = wm;
     }
-    if (warm && C.delay > 0.0) {
-        // transport-delay compensation (nmpf_node.cpp:206-221): predict the
-        // measured kite state over `delay` under the previous u(t0); theta,
-        // thetadot from the previous trajectory at t0 + delay
-        const double up[NU] = {Ub[0], Ub[1], Ub[2], 0.0};
-        double xp[NX];
-        rk4_primal(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp);
-        for (int i = 0; i < 13; ++i) x0[i] = xp[i];
-        x0[13] = Xb[C.delay_node * NX + 13];
-        x0[14] = Xb[C.delay_node * NX + 14];
+    __syncthreads();
+    const bool wm = sWarm != 0;
+    if (wm && C.shift) {
+        // in-place shift by one node / one interval, the last duplicated: every
+        // load of the wave is issued (and waited for) before its first store
+        constexpr int XS = (KITE_NMAX * NX + 63) / 64, US = (KITE_NMAX * NU + 63) / 64;
+        double xv[XS], uv[US];
+#pragma unroll
+        for (int q = 0; q < XS; ++q) {
+            const int e = l + 64 * q;
+            xv[q] = e < N * NX ? Xb[NX + e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < US; ++q) {
+            const int e = l + 64 * q;
+            uv[q] = e < (N - 1) * NU ? Ub[NU + e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < XS; ++q) {
+            const int e = l + 64 * q;
+            if (e < N * NX) Xb[e] = xv[q];
+        }
+#pragma unroll
+        for (int q = 0; q < US; ++q) {
+            const int e = l + 64 * q;
+            if (e < (N - 1) * NU) {
+                Ub[e] = uv[q];
+                if (e % NU == 3) sUv[e / NU] = uv[q];
+            }
+        }
+        if (l == 0) sUv[N - 1] = Ub[(N - 1) * NU + 3];      // the last interval keeps its control
     }
-    const double twopi = 2.0 * M_PI;
-    if (x0[13] > twopi) { x0[13] -= twopi; st |= 16; }
-    else if (x0[13] < -twopi) { x0[13] += twopi; st |= 16; }
-    if (x0[0] < C.min_speed) { x0[0] = C.min_speed; st |= 4; }
-    if (!warm) {
-        for (int k = 0; k < N; ++k)
-            for (int j = 0; j < NU; ++j) Ub[k * NU + j] = 0.5 * (C.lbu[j] + C.ubu[j]);
-        for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
-        for (int k = 0; k < N; ++k) rk4_primal(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX]);
-    } else if (C.shift) {
-        for (int k = 0; k < N; ++k)
-            for (int i = 0; i < NX; ++i) Xb[k * NX + i] = Xb[(k + 1) * NX + i];
-        for (int k = 0; k + 1 < N; ++k)
-            for (int j = 0; j < NU; ++j) Ub[k * NU + j] = Ub[(k + 1) * NU + j];
+    __syncthreads();
+    if (l < NX) Xb[l] = sx0[l];
+    if (l == 0) {
+        double th = sx0[13], thd = sx0[14];
+        for (int k = 0; k < N; ++k) {
+            const double uv = sUv[k];
+            const double thn = th + C.dt * thd + 0.5 * C.dt * C.dt * uv;
+            const double thdn = thd + C.dt * uv;
+            Xb[(k + 1) * NX + 13] = thn;
+            Xb[(k + 1) * NX + 14] = thdn;
+            th = thn; thd = thdn;
+        }
+        status[b] = st;
     }
-    for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
-    double th = x0[13], thd = x0[14];
-    for (int k = 0; k < N; ++k) {
-        const double uv = Ub[k * NU + 3];
-        const double thn = th + C.dt * thd + 0.5 * C.dt * C.dt * uv;
-        const double thdn = thd + C.dt * uv;
-        Xb[(k + 1) * NX + 13] = thn;
-        Xb[(k + 1) * NX + 14] = thdn;
-        th = thn; thd = thdn;
-    }
-    status[b] = st;
 }
 
 // ---------------------------------------------------------------------------
@@ -1484,7 +1528,7 @@ __global__ __launch_bounds__(64, 2) void k_closest_point(RtiConst C, int count, 
 // ---------------------------------------------------------------------------
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
                            double* X, double* U, int32_t* status, hipStream_t s) {
-    hipLaunchKernelGGL(k_prologue, dim3((B + 63) / 64), dim3(64), 0, s, P, C, B, warm, x0, X, U, status);
+    hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status);
     return hipGetLastError();
 }
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
