@@ -1,5 +1,7 @@
 #!/bin/bash
 # One GPU session: parity tests, benches, rocprofv3 kernel stats + HBM PMC passes.
+# The kernel-trace run uses the bench line's own arguments (--steps 30 --warmup 3),
+# so its steady-state means (profiles/<tag>_kernel_steady.json) compare 1:1.
 # Usage (on the GPU box, repo root): bash tools/gpu_round.sh TAG [QP_KERNEL]
 set -o pipefail
 TAG=${1:-r01}; QK=${2:-0}
@@ -7,7 +9,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 900 python -m pytest tests -m gpu -x -q -s > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
 timeout -k 10 300 python bench.py --steps 30 --warmup 3 --cpu-seconds 10 --qp-kernel $QK > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --qp-kernel $QK > $OUT/prof_bench.log 2>&1 || { echo "rocprof failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o fetch --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o write --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
-timeout -k 10 60 python tools/pmc_summary.py $OUT $TAG > $OUT/pmc_summary.log 2>&1 && cp profiles/${TAG}_* $OUT/ ; echo done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o ktrace --output-format csv -- python bench.py --steps 30 --warmup 3 --no-cpu-baseline --qp-kernel $QK > $OUT/prof_bench.log 2>&1 || { echo "rocprof failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o fetch --output-format csv -- python bench.py --steps 30 --warmup 3 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o write --output-format csv -- python bench.py --steps 30 --warmup 3 --no-cpu-baseline --qp-kernel $QK > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
+KITE_PROF_WARMUP=3 timeout -k 10 60 python tools/pmc_summary.py $OUT $TAG > $OUT/pmc_summary.log 2>&1 && cp profiles/${TAG}_* $OUT/ ; echo done

@@ -20,6 +20,22 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(REPO, "profiles")
 os.makedirs(prof, exist_ok=True)
 shutil.copy(os.path.join(src, "prof", "ktrace_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+# steady-state launch durations from the same trace: the profiled bench runs
+# WARMUP untimed steps first (cold-start QPs iterate longer), so the stats
+# mean over all launches sits above bench.py's HIP-event mean of the timed
+# steps; this drops the first WARMUP launches of each RTI kernel
+WARMUP = int(os.environ.get("KITE_PROF_WARMUP", "2"))
+durs = collections.defaultdict(list)
+for r in csv.DictReader(open(os.path.join(src, "prof", "ktrace_kernel_trace.csv"))):
+    durs[r["Kernel_Name"].split("(")[0]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+steady = {}
+for k, v in durs.items():
+    if k.startswith("k_") and len(v) > WARMUP:
+        st = v[WARMUP:]
+        steady[k] = {"launches": len(v), "mean_ns_all": sum(v) / len(v), "warmup_dropped": WARMUP,
+                     "mean_ns_steady": sum(st) / len(st), "min_ns": min(st), "max_ns": max(st)}
+json.dump({"tag": tag, "source": "rocprofv3 --kernel-trace (ktrace_kernel_trace.csv)", "kernels": steady},
+          open(os.path.join(prof, f"{tag}_kernel_steady.json"), "w"), indent=1)
 out = {}
 for sub, name, ctr in [("pmc_fetch", "fetch", "FETCH_SIZE"), ("pmc_write", "write", "WRITE_SIZE")]:
     vals = collections.defaultdict(list)
@@ -28,14 +44,16 @@ for sub, name, ctr in [("pmc_fetch", "fetch", "FETCH_SIZE"), ("pmc_write", "writ
     for k, v in vals.items():
         if k.startswith("k_"):
             d = out.setdefault(k, {})
-            d[f"{ctr}_bytes_raw"] = sum(v) / len(v)
-            d["launches"] = len(v)
+            st = v[WARMUP:] if len(v) > WARMUP else v     # steady-state launches, as for the durations
+            d[f"{ctr}_bytes_raw"] = sum(st) / len(st)
+            d["launches"] = len(st)
 for k, d in out.items():
     d["read_bytes"] = 2.0 * d.get("FETCH_SIZE_bytes_raw", 0.0)
     d["write_bytes"] = d.get("WRITE_SIZE_bytes_raw", 0.0)
     d["traffic_bytes"] = d["read_bytes"] + d["write_bytes"]
 json.dump({"tag": tag,
-           "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- python bench.py --steps 2 --warmup 1",
+           "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- python bench.py --steps 30 --warmup 3",
+           "warmup_launches_dropped": WARMUP,
            "correction": "read = 2 x FETCH_SIZE (gfx950 coalesced-read rule), write = WRITE_SIZE; per launch",
            "kernels": out}, open(os.path.join(prof, f"{tag}_pmc_hbm.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
