@@ -1407,7 +1407,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         rchi = row_lane && has_hi ? -q.shi * q.zhi - Da.dshi * Da.dzhi + sigma * mu : 0.0;
         Dir Dc;
         newton(rcl, rcu, rclo, rchi, Dc);
-        const double a = fmin(1.0, IPM_TAU * max_step(Dc));
+        const double a = fmin(1.0, fmax(IPM_TAU, 1.0 - mu) * max_step(Dc));   // tau_k -> 1 (oracle qp_ipm)
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             q.w[s] += a * Dc.dw[s];
