@@ -552,6 +552,12 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
     __shared__ double sG[2][4];                      // affine column rows 0, 6..8, by node parity
     __shared__ double sX[(NMAX + 1) * NX];           // linearisation trajectory
     __shared__ double sPth[NMAX + 1][6];             // P(theta_k), dP/dtheta(theta_k)
+    // vx-bound rows on the kite controls, staged for one bulk store after the
+    // node loop (short horizons; the long ones keep per-node stores: LDS)
+    constexpr bool STAGE_C = NR <= 6;           // LDS <= 38 KB: still 4 blocks per CU
+    constexpr int CLD = 3 * NMAX;
+    __shared__ double sCr[STAGE_C ? NMAX * CLD : 1];
+    __shared__ double sCl[STAGE_C ? NMAX : 1], sCu[STAGE_C ? NMAX : 1];
     __shared__ double sMax[4];
     // per-variable column scaling D, R diagonal and R ubar of the output
     // stage (a table: lane-dependent selects over kernel-argument fields
@@ -713,13 +719,18 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
         }
         // vx bound rows (node k >= 1)
         if (k >= 1) {
-            double* crow = Cr + ((size_t)b * N + (k - 1)) * n;
-            if (kite_lane) crow[t] = v[0] * Dl;
-            if (t < N + 2) crow[3 * N + t] = 0.0;
-            if (t == 0) {
-                const double base = xk[0] + g0;
-                cl[(size_t)b * N + k - 1] = C.lo_fin ? (C.lbx[0] - base) : -INFINITY;
-                cu[(size_t)b * N + k - 1] = C.hi_fin ? (C.ubx[0] - base) : INFINITY;
+            const double cv = v[0] * Dl;
+            const double base = xk[0] + g0;
+            const double clv = C.lo_fin ? (C.lbx[0] - base) : -INFINITY;
+            const double cuv = C.hi_fin ? (C.ubx[0] - base) : INFINITY;
+            if constexpr (STAGE_C) {
+                if (kite_lane) sCr[(k - 1) * CLD + t] = cv;
+                if (t == 0) { sCl[k - 1] = clv; sCu[k - 1] = cuv; }
+            } else {
+                double* crow = Cr + ((size_t)b * N + (k - 1)) * n;
+                if (kite_lane) crow[t] = cv;
+                if (t < N + 2) crow[3 * N + t] = 0.0;
+                if (t == 0) { cl[(size_t)b * N + k - 1] = clv; cu[(size_t)b * N + k - 1] = cuv; }
             }
         }
         if (last) {
@@ -785,6 +796,15 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
         node(k0 + 1, pf[1]);
     }
     __syncthreads();
+
+    // vx-bound rows C (kite-control columns from sCr, the rest zero) and their bounds
+    if constexpr (STAGE_C) {
+        for (int e = t; e < N * n; e += NT) {
+            const int r = e / n, c = e % n;
+            Cr[(size_t)b * N * n + e] = c < 3 * N ? sCr[r * CLD + c] : 0.0;
+        }
+        if (t < N) { cl[(size_t)b * N + t] = sCl[t]; cu[(size_t)b * N + t] = sCu[t]; }
+    }
 
     // write the scaled QP: Hs = D (H + Rdiag) D, hs = D (g + Rdiag ubar).
     // tiled != 0 (k_qp_tiled N = 20, k_qp_lds N = 40): the control block H_aa (na = 4N = 16*NT)
