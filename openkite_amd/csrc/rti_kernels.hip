@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
 // 128-lane blocks -> 4 blocks = 8 waves per CU in 160 KiB).
 constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances x 16 dirs
 #ifndef KITE_RK_OCC
-#define KITE_RK_OCC 2                     // launch_bounds occupancy hint of k_rk4_sens
+#define KITE_RK_OCC 1                     // launch_bounds occupancy hint of k_rk4_sens (1: 512 regs, no scratch spill)
 #endif
 constexpr int RK_LDS = 3 * NK;            // x.v, x.t, acc.t
 // DT: dual number (Dual fp64 / DualF fp32 for config.sens_fp32), ST: its scalar
