@@ -6,12 +6,15 @@ instances per GPU, N = 20 shooting intervals (tf = 1 s), M = 2 RK4 substeps,
 full fp64 RTI (shift -> RK4 + forward sensitivities -> Gauss-Newton
 condensing with fp64 MFMA -> interior-point QP -> expansion) per step.
 Synthetic, seeded instances; closed loop: the next step's
-measured state is the predicted state at t0 + dt of the current solution.
+measured state is the predicted state at t0 + dt of the current solution
+(openkite_amd/fleet.py).
 
 One process per GPU (torch.distributed / RCCL); the batch shards with no
 data-path collective (weak scaling); after each step the per-instance
 results (u0 + mpc_diagnostic) are all-gathered over RCCL, as a controller
-fleet would publish them.
+fleet would publish them.  ``--gpus N`` without a launcher starts the N
+ranks itself (torch.distributed.run as a child process, before this process
+touches a GPU) and fails if the node has fewer than N GPUs.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task).
 """
@@ -21,6 +24,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,9 +36,10 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP64_TFLOPS = 78.6        # MI355X fp64 vector = fp64 matrix (AMD spec)
 PEAK_HBM_GBS = 8000.0
+METRIC = "NMPC RTI steps/sec, batch=4096 N=20 horizon, 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -50,7 +56,9 @@ def parse():
                     help="fuse the EKF estimate (kiteEKF.cpp) before every RTI step (BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
-    return ap.parse_args()
+    ap.add_argument("--latency-steps", type=int, default=1000,
+                    help="warm single-kite steps of the single-thread CPU latency (BASELINE config 1)")
+    return ap.parse_args(argv)
 
 
 def synthetic_x0(B, offset, ctx):
@@ -75,21 +83,50 @@ def synthetic_x0(B, offset, ctx):
     return x
 
 
+def host_cpu_info():
+    """What the CPU numbers ran on: the machine's CPUs, this process's CPU set
+    and cgroup quota, and the thread count the box allots (OMP_NUM_THREADS)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            quota = None if q == "max" else round(int(q) / int(p), 2)
+    except Exception:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return dict(model=model, nproc=os.cpu_count(), affinity_cpus=affinity, cgroup_cpu_quota=quota,
+                omp_num_threads=int(omp) if omp and omp.isdigit() else None)
+
+
 def cpu_baseline(args, x0_host, budget_s):
     """The CPU oracle (oracle/kite_oracle.cpp, OpenMP over instances) on a
     bounded sample of the same workload: same instances, cold start + warm
-    closed-loop steps, same N/M/K.  Returns the dict for the JSON line."""
+    closed-loop steps, same N/M/K; plus the single-thread, batch-1 latency
+    (BASELINE config 1).  The reference's own CasADi/IPOPT path cannot run
+    here; these are the build's restatement of the RTI."""
     from oracle import ffi
+    info = host_cpu_info()
+    # the threads this job may use: the box allots OMP_NUM_THREADS CPUs to a
+    # one-GPU job (nproc shows the whole machine); else this process's CPU set
+    threads = info["omp_num_threads"] or info["affinity_cpus"] or os.cpu_count() or 1
     kp = ffi.load_params()
     cfgv = ffi.cfg_vector(ffi.node_config(N=args.horizon))
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except Exception:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(threads, 16))
+    N = args.horizon
     S = min(x0_host.shape[0], 64 * threads)
     x = x0_host[:S].copy()
-    N = args.horizon
     X = np.zeros((S, N + 1, 15)); U = np.zeros((S, N, 4))
     ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=0, nthreads=threads)
     x = X[:, 1, :].copy()
@@ -101,38 +138,95 @@ def cpu_baseline(args, x0_host, budget_s):
         el = time.perf_counter() - t0
         if (el >= budget_s and steps >= 2) or steps >= 200:
             break
+    # config 1: one kite, one thread, warm closed-loop steps; 40 kites x 25
+    # steps (each kite restarted cold, its cold step not timed)
+    lat, per_kite = [], 25
+    kites = max(1, (args.latency_steps + per_kite - 1) // per_kite)
+    X1 = np.zeros((1, N + 1, 15)); U1 = np.zeros((1, N, 4))
+    for k in range(kites):
+        x1 = x0_host[k % x0_host.shape[0]][None].copy()
+        ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x1, X1, U1, warm=0, nthreads=1)
+        for _ in range(per_kite):
+            x1 = X1[:, 1, :].copy()
+            t = time.perf_counter()
+            ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x1, X1, U1, warm=1, nthreads=1)
+            lat.append(time.perf_counter() - t)
+    lat = np.array(lat[:args.latency_steps]) * 1e3
     return dict(value=S * steps / el, unit="RTI steps/s", cores=threads, kind="port",
                 sample=f"{S} instances x {steps} warm closed-loop RTI steps (N={N}, M={args.substeps}, "
-                       f"K<={args.qp_iters}), oracle/kite_oracle.cpp -O3 OpenMP {threads} threads, {el:.1f} s")
+                       f"K<={args.qp_iters}), oracle/kite_oracle.cpp -O3 OpenMP {threads} threads, {el:.1f} s; "
+                       "the reference's CasADi/IPOPT path cannot be built or run here (SURVEY.md 8(c))",
+                host=info,
+                latency_1thread_batch1=dict(median_ms=round(float(np.median(lat)), 4),
+                                            p05_ms=round(float(np.percentile(lat, 5)), 4),
+                                            p95_ms=round(float(np.percentile(lat, 95)), 4),
+                                            steps=int(lat.size), rti_per_s=round(1e3 / float(np.median(lat)), 1),
+                                            note=f"BASELINE configs[0] analogue: one kite, one thread, warm "
+                                                 f"closed-loop steps ({kites} kites x {per_kite})"))
 
 
-def pmc_traffic(kernel):
+def run_config_tag(args):
+    return dict(batch=args.batch, N=args.horizon, M=args.substeps, K=args.qp_iters,
+                fp32_sens=bool(args.fp32_sens), ekf=bool(args.ekf), qp_kernel=args.qp_kernel)
+
+
+def pmc_traffic(kernel, cfg_tag):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<round>_pmc_hbm.json, written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    (profiles/<round>_pmc_hbm.json, tools/pmc_summary.py) whose recorded bench
+    configuration is this run's; None if no profile matches."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
     for f in reversed(files):
-        d = json.load(open(f)).get("kernels", {})
-        for name in (f"k_{kernel}_tiled", f"k_{kernel}"):
-            if name in d and "traffic_bytes" in d[name]:
-                return d[name]["traffic_bytes"], os.path.relpath(f, ROOT) + f" ({name})"
-    return None, "no PMC summary"
+        d = json.load(open(f))
+        if d.get("bench_config") != cfg_tag:
+            continue
+        ks = d.get("kernels", {})
+        for name in sorted(ks):
+            if name.split("<")[0] in (f"k_{kernel}_tiled", f"k_{kernel}_lds", f"k_{kernel}") and \
+                    "traffic_bytes" in ks[name]:
+                return ks[name]["traffic_bytes"], os.path.relpath(f, ROOT) + f" ({name})"
+    return None, "no PMC summary of this configuration"
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without a launcher: start N ranks (one per GPU) as a child
+    torch.distributed.run, before this process touches any GPU."""
+    import torch
+    have = torch.cuda.device_count()          # does not initialise the GPU on this image
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} requested but this node has {have} GPU(s)", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+
     import torch
     import torch.distributed as dist
     import openkite_amd as ok
     from openkite_amd import flops
+    from openkite_amd.fleet import FleetLoop, GpuStepper
     from openkite_amd.shard import Publisher, max_over_ranks, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -149,44 +243,12 @@ def main():
     offset, count = shard(world * B, world, rank)      # weak scaling: B instances per GPU
     assert count == B
     x0_host = synthetic_x0(B, offset, ctx)
-    d_x0 = torch.from_numpy(x0_host).to(dev)
-    d_u0 = torch.zeros((B, 4), dtype=torch.float64, device=dev)
-    d_traj = torch.zeros((B, N + 1, 15), dtype=torch.float64, device=dev)
-    d_diag = torch.zeros((B, 6), dtype=torch.float64, device=dev)
-    d_status = torch.zeros((B,), dtype=torch.int32, device=dev)
     pub = Publisher(B, dev, world) if world > 1 and not args.no_allgather else None
-
-    if args.ekf:
-        W, V, P0 = ok.ekf_default_covariances()
-        d_W = torch.from_numpy(W).to(dev); d_V = torch.from_numpy(V).to(dev)
-        d_P = torch.from_numpy(np.repeat(P0[None], B, axis=0)).to(dev)
-        d_xe = d_x0[:, :13].clone()
-        d_u3 = torch.zeros((B, 3), dtype=torch.float64, device=dev)
-        d_z = d_x0[:, 6:13].clone()
-
-    def one_step():
-        if args.ekf:
-            # estimator (kiteEKF.cpp:75-126): propagate under the applied control,
-            # update with the measured position + attitude of the plant (here the
-            # model's own prediction), then the RTI from the estimate
-            # (propagation in 5 steps of dt/5: one RK4 step of 0.05 s is too coarse
-            # for the tether dynamics; the reference estimator runs at the
-            # measurement rate)
-            d_u3.copy_(d_u0[:, :3])
-            for j in range(5):
-                ctx.ekf_step_device(B, cfg.dt / 5, d_xe.data_ptr(), d_u3.data_ptr(), d_P.data_ptr(),
-                                    d_z.data_ptr() if j == 4 else 0, d_W.data_ptr(), d_V.data_ptr())
-            d_x0[:, :13].copy_(d_xe)
-        ctx.step_device(d_x0.data_ptr(), d_u0.data_ptr(), d_traj.data_ptr(), 0, d_diag.data_ptr(),
-                        d_status.data_ptr())
-        if args.ekf:
-            d_z.copy_(d_traj[:, 1, 6:13])
-        if pub is not None:
-            pub.publish(d_u0, d_diag)          # all ranks see every kite's u0 + diagnostics
-        d_x0.copy_(d_traj[:, 1, :])        # closed loop: predicted state at t0 + dt
+    loop = FleetLoop(GpuStepper(ctx), torch.from_numpy(x0_host).to(dev), N, cfg.dt, ekf=args.ekf,
+                     covariances=ok.ekf_default_covariances() if args.ekf else None, publisher=pub)
 
     for _ in range(args.warmup):
-        one_step()
+        loop.step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -194,7 +256,7 @@ def main():
     ctx.timing_start(args.steps)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        one_step()
+        loop.step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -203,7 +265,7 @@ def main():
     nrec, ksum = ctx.timing_read()
     kkt, iters = ctx.qp_stats()
     it_sum = ctx.qp_iteration_sum()
-    status = d_status.cpu().numpy()
+    status = loop.status.cpu().numpy()
 
     elapsed_max = max_over_ranks(elapsed, dev)
     total_rti = world * B * args.steps
@@ -220,7 +282,7 @@ def main():
         dom_flops = fl.get(dom, 0.0) * B
         achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
-        traffic, tsrc = pmc_traffic(dom)
+        traffic, tsrc = pmc_traffic(dom, run_config_tag(args))
         roofline = dict(bound="mfma", achieved=round(achieved, 4), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic, kernel=dom,
                         note="fp64 compute roof (vector = matrix peak on gfx950); achieved = algorithmic flops "
@@ -229,8 +291,12 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, x0_host, args.cpu_seconds)
+        workload = (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
+                    + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
+                    + (" + fused EKF (BASELINE configs[4])" if args.ekf else
+                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens else ""))
         out = {
-            "metric": "NMPC RTI steps/sec, batch=4096 N=20 horizon, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "RTI steps/s",
             "n_gpus": world,
@@ -242,21 +308,20 @@ def main():
             "vs_baseline": None,
             "dtype": "f64" if not args.fp32_sens else "f64 (f32 sensitivities)",
             "data": "synthetic (seeded perturbations of launch/simulator.launch:3, umx_radian params)",
-            "config": {"workload": (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
-                                    + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
-                                    + (" + fused EKF (BASELINE configs[4])" if args.ekf else
-                                       " (BASELINE configs[2])" if N == 20 else "")),
-                       "ekf": bool(args.ekf),
+            "config": {"workload": workload, "ekf": bool(args.ekf),
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
                        "allgather": bool(world > 1 and not args.no_allgather)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items()},
+            "interval_integrations_per_s": round(world * B * N / (avg_ms["rk4_sens"] * 1e-3), 1)
+            if avg_ms["rk4_sens"] > 0 else None,
             "rti_tflops_all_kernels": round(rti_flops, 4),
             "qp_mean_iterations": round(mean_it, 3),
             "qp_converged_frac": round(float(np.mean(kkt < 1e-8)), 5),
             "status_nan": int(np.sum(status & 1)),
+            "run_config": run_config_tag(args),
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -8,14 +8,23 @@
 // Differences kept deliberately visible:
 //   * the OCP is fixed at createNLP() (an RTI context), setters before it
 //     configure, bound setters after it update the live context;
-//   * getOptimalControl()/getOptimalTrajetory() keep the reference's REVERSED
-//     time order (last column = t0, nmpf_node.cpp:124 reads column N);
-//   * getStats() returns the IPOPT-style return_status string only;
+//   * getOptimalControl()/getOptimalTrajetory() keep the reference's shapes
+//     (4 x (N+1), 15 x (N+1)) and REVERSED time order (last column = t0,
+//     nmpf_node.cpp:124 reads column N).  The RTI has N piecewise-constant
+//     controls (interval k starts at node k); column 0 (t = tf, where no
+//     interval starts) repeats u_{N-1}, the control held up to tf;
+//   * getStats() returns a string map (kite_amd::Dict) holding the IPOPT-style
+//     "return_status" the node reads (nmpf_node.cpp:222-223), plus the RTI's
+//     status bits;
+//   * getPathFunction() returns a callable theta -> {x, y, z} instead of a
+//     casadi::Function (nmpf_node.cpp:177-179 evaluates it per node);
 //   * initialized() mirrors the reference, which never sets it (kiteNMPF.cpp:46).
 #pragma once
 
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -37,6 +46,10 @@ private:
 inline void kite_check(int rc, const char* what) {
     if (rc < 0) throw KiteNmpcError(rc, what);
 }
+
+// casadi::Dict stand-in for getStats(): stats["return_status"] reads as in
+// nmpf_node.cpp:222-223
+using Dict = std::map<std::string, std::string>;
 
 // KiteDynamics stand-in: the parameter set (kite_utils::LoadProperties, kite.cpp:7-76)
 inline kite_params LoadProperties(const std::string& yaml_path) {
@@ -102,12 +115,15 @@ public:
     }
 
     // ---- getters (kiteNMPF.h:42-60) -----------------------------------------
-    // 4 x N, column-major, reference column order: last column = u(t0)
+    // 4 x (N+1), column-major, reference shape and column order: column N - k
+    // = u_k, so the last column is u(t0); column 0 (t = tf) repeats u_{N-1}
     std::vector<double> getOptimalControl() const {
         const int N = cfg_.N;
-        std::vector<double> out((size_t)4 * N);
-        for (int k = 0; k < N; ++k)
-            for (int c = 0; c < 4; ++c) out[(size_t)(N - 1 - k) * 4 + c] = ctrl_.empty() ? 0.0 : ctrl_[k * 4 + c];
+        std::vector<double> out((size_t)4 * (N + 1));
+        for (int k = 0; k <= N; ++k) {
+            const int src = k < N ? k : N - 1;
+            for (int c = 0; c < 4; ++c) out[(size_t)(N - k) * 4 + c] = ctrl_.empty() ? 0.0 : ctrl_[src * 4 + c];
+        }
         return out;
     }
     // 15 x (N+1), column-major, reference column order: last column = x(t0)
@@ -118,12 +134,24 @@ public:
             for (int i = 0; i < 15; ++i) out[(size_t)(N - k) * 15 + i] = traj_.empty() ? 0.0 : traj_[k * 15 + i];
         return out;
     }
-    // "return_status" of getStats() (kiteNMPF.cpp:303-313)
-    std::string getStats() const {
-        if (status_ & KITE_ST_NAN) return "Invalid_Number_Detected";
-        if (status_ & KITE_ST_STEP_REJECTED) return "Restoration_Failed";
-        if (status_ & KITE_ST_QP_NOT_CONV) return "Maximum_Iterations_Exceeded";
-        return "Solve_Succeeded";
+    // getStats() (kiteNMPF.h:48): "return_status" as IPOPT names it
+    // (kiteNMPF.cpp:303-313 checks these strings) + the RTI status bits
+    Dict getStats() const {
+        const char* rs = "Solve_Succeeded";
+        if (status_ & KITE_ST_NAN) rs = "Invalid_Number_Detected";
+        else if (status_ & KITE_ST_STEP_REJECTED) rs = "Restoration_Failed";
+        else if (status_ & KITE_ST_QP_NOT_CONV) rs = "Maximum_Iterations_Exceeded";
+        return Dict{{"return_status", rs}, {"status_bits", std::to_string(status_)}};
+    }
+    // getPathFunction() (kiteNMPF.h:46): P(theta) of the configured path
+    // (the rotated circle of nmpf_node.cpp:30-40), evaluated on the host
+    std::function<std::vector<double>(double)> getPathFunction() const {
+        const kite_nmpc_config cfg = cfg_;
+        return [cfg](double theta) {
+            std::vector<double> P(3);
+            kite_check(kite_nmpc_path_eval(&cfg, 1, &theta, P.data(), nullptr), "getPathFunction");
+            return P;
+        };
     }
     int32_t statusBits() const { return status_; }
     double getPathError() const { return diag_.pos_error; }

@@ -165,6 +165,14 @@ int kite_nmpc_synchronize(kite_nmpc_ctx* ctx);
  * positions (count x 3); guess may be NULL (= 0 as in the reference).       */
 int kite_nmpc_closest_point(kite_nmpc_ctx* ctx, int32_t count, const double* pos,
                             const double* guess, double* theta_out);
+/* getPathFunction (kiteNMPF.h:46; the path built at nmpf_node.cpp:30-40 and
+ * evaluated per trajectory node for /opt_traj at nmpf_node.cpp:177-183):
+ * P(theta) = vec(q^-1 (x) [0, R cos, R sin, alt] (x) q) and dP/dtheta for
+ * `count` angles (count x 3 each; dP3 may be NULL).  Host arithmetic on the
+ * configuration only (no context, no GPU): a visualisation helper of the
+ * node, not part of the RTI step.                                           */
+int kite_nmpc_path_eval(const kite_nmpc_config* cfg, int32_t count, const double* theta,
+                        double* P3, double* dP3);
 
 /* One RTI step for the whole batch: replaces KiteNMPF::computeControl
  * (kiteNMPF.cpp:199-316) -- NLP_Solver(ARG) becomes shift -> rk4_sens ->
@@ -199,9 +207,11 @@ int kite_nmpc_jacobian(kite_nmpc_ctx* ctx, int32_t count, const double* x13,
  * substeps over tf: the delay-compensation predictor of nmpf_node.cpp:218.   */
 int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
                       const double* u4, double tf, int32_t steps, double* x15_out);
-/* The hot kernel alone: x+ and S = dx+/d[x,u] over one shooting interval
- * (h = tf/M, M substeps).  count x 15, count x 4 -> count x 15, count x 15 x 15,
- * count x 15 x 4.                                                           */
+/* The hot kernel alone (k_rk4_sens on `count` one-interval horizons, BASELINE
+ * config 2): x+ and S = dx+/d[x,u] over one shooting interval (h = tf/M, M
+ * substeps).  count x 15, count x 4 -> count x 15, count x 15 x 15,
+ * count x 15 x 4.  Sensitivities in fp32 (x+ in fp64) when the context was
+ * created with config.sens_fp32 = 1.                                        */
 int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
                        const double* u4, double tf, int32_t M, double* xnext,
                        double* A, double* B);

@@ -743,9 +743,13 @@ int kite_nmpc_rk4_sens(kite_nmpc_ctx* ctx, int32_t count, const double* x15, con
     if (!ctx || count < 1 || !x15 || !u4 || !xnext || !A || !Bm || M < 1 || !std::isfinite(tf)) return KITE_EINVAL;
     const size_t c = count;
     const double h = tf / M;
-    return run_items(ctx, {{x15, c * 15}, {u4, c * 4}}, {{xnext, c * 15}, {A, c * 225}, {Bm, c * 60}},
+    // scratch outputs (no host copy): X2 [c][2][15], AB [c][13][16], DEF [c][13]
+    return run_items(ctx, {{x15, c * 15}, {u4, c * 4}},
+                     {{xnext, c * 15}, {A, c * 225}, {Bm, c * 60}, {nullptr, c * 30}, {nullptr, c * 208},
+                      {nullptr, c * 13}},
                      [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
-                         return kite::launch_rk4_sens_items(ctx->mc, count, M, h, i[0], i[1], o[0], o[1], o[2], s);
+                         return kite::launch_rk4_sens_items(ctx->mc, ctx->rc.sens_fp32, count, M, h, i[0], i[1],
+                                                            o[0], o[1], o[2], o[3], o[4], o[5], s);
                      });
 }
 
@@ -759,6 +763,27 @@ int kite_nmpc_closest_point(kite_nmpc_ctx* ctx, int32_t count, const double* pos
                      [&](std::vector<double*>& i, std::vector<double*>& o, hipStream_t s) {
                          return kite::launch_closest_point(ctx->rc, count, i[0], i[1], o[0], s);
                      });
+}
+
+int kite_nmpc_path_eval(const kite_nmpc_config* cfg, int32_t count, const double* theta, double* P3, double* dP3) {
+    if (!cfg || count < 0 || (count > 0 && (!theta || !P3))) return KITE_EINVAL;
+    // rotation by the unit quaternion (w, u): v' = (w^2 - u.u) v + 2 (u.v) u - 2 w (u x v)
+    // (q^-1 (x) [0, v] (x) q, the sandwich of nmpf_node.cpp:35-39)
+    const double w = cfg->path_q[0], ux = cfg->path_q[1], uy = cfg->path_q[2], uz = cfg->path_q[3];
+    const double ww_uu = w * w - (ux * ux + uy * uy + uz * uz);
+    auto rot = [&](double vx, double vy, double vz, double* out) {
+        const double ud = ux * vx + uy * vy + uz * vz;
+        const double cx = uy * vz - uz * vy, cy = uz * vx - ux * vz, cz = ux * vy - uy * vx;
+        out[0] = ww_uu * vx + 2.0 * ud * ux - 2.0 * w * cx;
+        out[1] = ww_uu * vy + 2.0 * ud * uy - 2.0 * w * cy;
+        out[2] = ww_uu * vz + 2.0 * ud * uz - 2.0 * w * cz;
+    };
+    for (int32_t i = 0; i < count; ++i) {
+        const double s = std::sin(theta[i]), c = std::cos(theta[i]);
+        rot(cfg->path_radius * c, cfg->path_radius * s, cfg->path_altitude, P3 + 3 * (size_t)i);
+        if (dP3) rot(-cfg->path_radius * s, cfg->path_radius * c, 0.0, dP3 + 3 * (size_t)i);
+    }
+    return KITE_OK;
 }
 
 int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n) {

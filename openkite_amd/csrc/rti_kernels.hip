@@ -251,8 +251,10 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
     __syncthreads();
     const bool wm = sWarm != 0;
     if (wm && C.shift) {
-        // in-place shift by one node / one interval, the last duplicated: every
-        // load of the wave is issued (and waited for) before its first store
+        // in-place shift by one node / one interval, the last duplicated: all
+        // loads of the wave complete before any store (the barrier's fence
+        // orders them for the compiler and the memory pipeline; lane l stores
+        // elements other lanes loaded)
         constexpr int XS = (KITE_NMAX * NX + 63) / 64, US = (KITE_NMAX * NU + 63) / 64;
         double xv[XS], uv[US];
 #pragma unroll
@@ -265,6 +267,7 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
             const int e = l + 64 * q;
             uv[q] = e < (N - 1) * NU ? Ub[NU + e] : 0.0;
         }
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < XS; ++q) {
             const int e = l + 64 * q;
@@ -305,10 +308,11 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
 // column of [A_k | B_k]; lane 0 of each instance writes the defect.
 // ---------------------------------------------------------------------------
 // Classic RK4 (M substeps) on value + one tangent.  One dual RHS needs ~166
-// VGPRs, so the RK4 state cannot stay in registers at 2 waves/SIMD: the
-// substep start state x (value+tangent) and the tangent half of the
-// accumulator live in LDS (SoA [component][lane], conflict-free, 312 B/lane;
-// 128-lane blocks -> 4 blocks = 8 waves per CU in 160 KiB).
+// VGPRs; the substep start state x (value+tangent) and the tangent half of
+// the accumulator live in LDS (SoA [component][lane], conflict-free,
+// 312 B/lane, 39 KiB per 128-lane block).  Occupancy: KITE_RK_OCC = 1 wave
+// per SIMD (512 registers): at 2 waves/SIMD the kernel spilled 160 B/lane to
+// scratch (same speed, 0.25 GB more HBM traffic per launch).
 constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances x 16 dirs
 #ifndef KITE_RK_OCC
 #define KITE_RK_OCC 1                     // launch_bounds occupancy hint of k_rk4_sens (1: 512 regs, no scratch spill)
@@ -1493,43 +1497,48 @@ __global__ __launch_bounds__(64, 2) void k_predict(ModelConst P, int count, cons
 }
 
 // rk4 with sensitivities for independent (x,u) items (API kite_nmpc_rk4_sens):
-// same lane mapping as k_rk4_sens; writes full 15x15 / 15x4 blocks with the
-// exact theta/thetadot/Uv rows and columns.
-__global__ __launch_bounds__(RK_T, 2) void k_rk4_sens_items(ModelConst P, int count, int M, double h,
-                                                           const double* __restrict__ x,
-                                                           const double* __restrict__ u,
-                                                           double* __restrict__ xo,
-                                                           double* __restrict__ A,
-                                                           double* __restrict__ Bm) {
-    __shared__ double xsh[RK_LDS][RK_T];
-    const int d = threadIdx.x & 15;
-    const int i = blockIdx.x * (RK_T / 16) + (threadIdx.x >> 4);
-    if (i >= count) return;
-    const double* xi = x + (size_t)i * NX;
-    const double* ui = u + (size_t)i * NU;
-    Dual xv[NK], uu[NKU];
-#pragma unroll
-    for (int j = 0; j < NK; ++j) xv[j] = mk(xi[j], d == j ? 1.0 : 0.0);
-#pragma unroll
-    for (int j = 0; j < NKU; ++j) uu[j] = mk(ui[j], d == NK + j ? 1.0 : 0.0);
-    rk4_dual(P, xv, uu, h, M, xsh, threadIdx.x);
+// the items run through the hot kernel k_rk4_sens itself as a batch of
+// one-interval horizons (N = 1, node 1 = 0 so the "defect" is x+), then
+// k_sens_items_expand writes the full 15x15 / 15x4 blocks with the exact
+// theta/thetadot/Uv rows and columns.  X2 [count][2][15] is scratch.
+__global__ __launch_bounds__(64) void k_sens_items_stage(int count, const double* __restrict__ x,
+                                                         double* __restrict__ X2) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= count * 2 * NX) return;
+    const int i = g / (2 * NX), e = g % (2 * NX);
+    X2[g] = e < NX ? x[(size_t)i * NX + e] : 0.0;
+}
+// lane per (item, row r of [A | B]): 15 rows per item
+__global__ __launch_bounds__(64) void k_sens_items_expand(int count, int M, double h, const double* __restrict__ x,
+                                                          const double* __restrict__ u,
+                                                          const double* __restrict__ AB,
+                                                          const double* __restrict__ DEF, double* __restrict__ xo,
+                                                          double* __restrict__ A, double* __restrict__ Bm) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= count * NX) return;
+    const int i = g / NX, r = g % NX;
     const double T = h * M;
-    double* Ai = A + (size_t)i * NX * NX;
-    double* Bi = Bm + (size_t)i * NX * NU;
-    for (int r = 0; r < NK; ++r) {
-        if (d < NK) Ai[r * NX + d] = xv[r].t;
-        else Bi[r * NU + (d - NK)] = xv[r].t;
-    }
-    if (d == 0) {
-        for (int r = 0; r < NK; ++r) { Ai[r * NX + 13] = 0.0; Ai[r * NX + 14] = 0.0; Bi[r * NU + 3] = 0.0; }
-        for (int c = 0; c < NX; ++c) { Ai[13 * NX + c] = 0.0; Ai[14 * NX + c] = 0.0; }
-        Ai[13 * NX + 13] = 1.0; Ai[13 * NX + 14] = T; Ai[14 * NX + 14] = 1.0;
-        for (int c = 0; c < NU; ++c) { Bi[13 * NU + c] = 0.0; Bi[14 * NU + c] = 0.0; }
-        Bi[13 * NU + 3] = 0.5 * T * T; Bi[14 * NU + 3] = T;
-        double* xoi = xo + (size_t)i * NX;
-        for (int r = 0; r < NK; ++r) xoi[r] = xv[r].v;
-        xoi[13] = xi[13] + T * xi[14] + 0.5 * T * T * ui[3];
-        xoi[14] = xi[14] + T * ui[3];
+    double* Ar = A + ((size_t)i * NX + r) * NX;
+    double* Br = Bm + ((size_t)i * NX + r) * NU;
+    const double* xi = x + (size_t)i * NX;
+    if (r < NK) {
+        const double* ab = AB + ((size_t)i * NK + r) * 16;
+        for (int c = 0; c < NK; ++c) Ar[c] = ab[c];
+        Ar[13] = 0.0; Ar[14] = 0.0;
+        for (int c = 0; c < NKU; ++c) Br[c] = ab[NK + c];
+        Br[3] = 0.0;
+        xo[(size_t)i * NX + r] = DEF[(size_t)i * NK + r];
+    } else {
+        for (int c = 0; c < NX; ++c) Ar[c] = 0.0;
+        for (int c = 0; c < NU; ++c) Br[c] = 0.0;
+        const double uv = u[(size_t)i * NU + 3];
+        if (r == 13) {
+            Ar[13] = 1.0; Ar[14] = T; Br[3] = 0.5 * T * T;
+            xo[(size_t)i * NX + 13] = xi[13] + T * xi[14] + 0.5 * T * T * uv;
+        } else {
+            Ar[14] = 1.0; Br[3] = T;
+            xo[(size_t)i * NX + 14] = xi[14] + T * uv;
+        }
     }
 }
 
@@ -1609,9 +1618,16 @@ hipError_t launch_predict(const ModelConst& P, int count, const double* x, const
     hipLaunchKernelGGL(k_predict, dim3((count + 63) / 64), dim3(64), 0, s, P, count, x, u, h, steps, xo);
     return hipGetLastError();
 }
-hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h, const double* x,
-                                 const double* u, double* xo, double* A, double* Bm, hipStream_t s) {
-    hipLaunchKernelGGL(k_rk4_sens_items, dim3((count + RK_T / 16 - 1) / (RK_T / 16)), dim3(RK_T), 0, s, P, count, M, h, x, u, xo, A, Bm);
+hipError_t launch_rk4_sens_items(const ModelConst& P, int sens_fp32, int count, int M, double h, const double* x,
+                                 const double* u, double* xo, double* A, double* Bm, double* X2, double* AB,
+                                 double* DEF, hipStream_t s) {
+    hipLaunchKernelGGL(k_sens_items_stage, dim3((count * 2 * NX + 63) / 64), dim3(64), 0, s, count, x, X2);
+    RtiConst C{};
+    C.N = 1; C.M = M; C.h = h; C.sens_fp32 = sens_fp32;
+    hipError_t e = launch_rk4_sens(P, C, count, X2, u, AB, DEF, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_sens_items_expand, dim3((count * NX + 63) / 64), dim3(64), 0, s, count, M, h, x, u, AB, DEF,
+                       xo, A, Bm);
     return hipGetLastError();
 }
 hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,

@@ -59,8 +59,9 @@ hipError_t launch_jacobian(const ModelConst& P, int count, const double* x, cons
                            double* Ju, hipStream_t s);
 hipError_t launch_predict(const ModelConst& P, int count, const double* x, const double* u, double h,
                           int steps, double* xo, hipStream_t s);
-hipError_t launch_rk4_sens_items(const ModelConst& P, int count, int M, double h, const double* x,
-                                 const double* u, double* xo, double* A, double* Bm, hipStream_t s);
+hipError_t launch_rk4_sens_items(const ModelConst& P, int sens_fp32, int count, int M, double h, const double* x,
+                                 const double* u, double* xo, double* A, double* Bm, double* X2, double* AB,
+                                 double* DEF, hipStream_t s);
 hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos, const double* guess,
                                 double* theta, hipStream_t s);
 // Chebyshev collocation evaluator (colloc_kernels.hip): constants of one formulation

@@ -9,7 +9,6 @@ fallback.
 from __future__ import annotations
 
 import ctypes
-import math
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -113,6 +112,7 @@ _SIGNATURES = {
     "kite_nmpc_use_own_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_closest_point": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP]),
+    "kite_nmpc_path_eval": (ctypes.c_int, [ctypes.POINTER(NmpcConfig), ctypes.c_int32, _DP, _DP, _DP]),
     "kite_nmpc_step": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP, ctypes.POINTER(MpcDiagnostic), _IP]),
     "kite_nmpc_step_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -404,6 +404,15 @@ class _ReturnStatus:
         return "Solve_Succeeded"
 
 
+def path_eval(config: NmpcConfig, theta):
+    """P(theta) and dP/dtheta of the configured path (kite_nmpc_path_eval:
+    getPathFunction, nmpf_node.cpp:30-40); host arithmetic, no GPU."""
+    th = _f64(theta).reshape(-1)
+    P = np.zeros((th.size, 3)); dP = np.zeros((th.size, 3))
+    _check(lib().kite_nmpc_path_eval(ctypes.byref(config), th.size, _p(th), _p(P), _p(dP)), "path_eval")
+    return P, dP
+
+
 def colloc_default_config(**overrides) -> CollocConfig:
     """The NMPF's collocation setup (kiteNMPF.cpp:80-143 + node scaling/path)."""
     c = CollocConfig()
@@ -547,22 +556,21 @@ class KiteNMPF:
         self.enableWarmStart()
 
     def getOptimalControl(self):
-        """4 x N, reference column order (last column = u(t0))."""
-        return None if self._ctrl is None else self._ctrl[::-1].T.copy()
+        """4 x (N+1), reference shape and column order: column N - k = u_k (last
+        column = u(t0)); column 0 (t = tf, where no interval starts) repeats
+        u_{N-1}, the control held up to tf."""
+        if self._ctrl is None:
+            return None
+        return np.vstack([self._ctrl, self._ctrl[-1:]])[::-1].T.copy()
 
     def getOptimalTrajetory(self):   # [sic] kiteNMPF.h:44
         """15 x (N+1), reference column order (last column = x(t0))."""
         return None if self._traj is None else self._traj[::-1].T.copy()
 
     def getPathFunction(self):
+        """theta -> P(theta) (3,) of the configured path (kiteNMPF.h:46)."""
         cfg = self._cfg
-        qw, qx, qy, qz = list(cfg.path_q)
-
-        def P(theta):
-            v = np.array([cfg.path_radius * math.cos(theta), cfg.path_radius * math.sin(theta), cfg.path_altitude])
-            u = np.array([qx, qy, qz])
-            return (qw * qw - u @ u) * v + 2 * (u @ v) * u - 2 * qw * np.cross(u, v)
-        return P
+        return lambda theta: path_eval(cfg, [theta])[0][0]
 
     def getStats(self):
         return {"return_status": _ReturnStatus(self._status).return_status, "status_bits": self._status}

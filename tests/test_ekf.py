@@ -51,6 +51,77 @@ def test_oracle_ekf_propagate_and_update(kp):
         assert np.trace(Pu[6:, 6:]) < np.trace(Pp[6:, 6:])
 
 
+def _ekf_reference():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ekf_reference.json")) as f:
+        return json.load(f)
+
+
+KP_LT, KP_KS, KP_KD = 46, 47, 48          # tether length / stiffness / damping in the oracle vector
+
+
+def test_oracle_ekf_vs_reference_expected_output(kp):
+    """The one expected numeric output the reference ships: kite_control_test.cpp
+    ekf_test (:46-86) runs KiteEKF::_estimate(measurement, dt = 0.0084) from
+    x_est with zero control and the default covariances and compares with a
+    MATLAB vector at inf-norm 0.01 (:84, commented out upstream).
+
+    Measured: the C++ model as configured by umx_radian.yaml misses the
+    vector by 0.27 in the body velocities.  At x_est the kite is 3.89 m from
+    the anchor, beyond the 2.81 m tether, so the spring-damper pulls 0.7 N on
+    a 44 g airframe (~32 m/s^2), while the MATLAB vector implies ~0.5 m/s^2:
+    the MATLAB data was produced with a slack or absent tether (the MATLAB
+    prototype's tether, kite_sim.m:213-226, differs from the C++ one).  With
+    the tether slack (Ks = Kd = 0, or any Lt beyond 3.89 m) the restatement
+    reproduces the MATLAB vector within the author's 0.01 -- this pins the
+    aerodynamics, gravity, kinematics, RK4 propagation, Jacobian-based
+    covariance propagation and the Kalman update against the reference's own
+    data; the tether term stays pinned by the 50-digit golden fixtures."""
+    r = _ekf_reference()
+    W, V, P0 = ok.ekf_default_covariances()
+    x, z, u = np.array(r["x_est"]), np.array(r["measurement"]), np.array(r["control"])
+    ref = np.array(r["reference_est"])
+    slack = kp.copy(); slack[KP_KS] = 0.0; slack[KP_KD] = 0.0
+    xs, _ = ffi.ekf_step(slack, x, u, r["dt"], P0, z, W, V)
+    assert np.abs(xs - ref).max() < r["tolerance_inf"], xs - ref
+    long_tether = kp.copy(); long_tether[KP_LT] = 10.0          # slack by geometry instead
+    xl, _ = ffi.ekf_step(long_tether, x, u, r["dt"], P0, z, W, V)
+    assert np.abs(xl - ref).max() < r["tolerance_inf"]
+    # the yaml tether: the miss is the tether impulse over dt, nothing else
+    xf, _ = ffi.ekf_step(kp, x, u, r["dt"], P0, z, W, V)
+    assert np.abs(xf - ref).max() > 0.1
+    # (first-order impulse dt * tether acceleration at x_est explains the miss
+    # to within 5 % of its size; the rest is RK4 vs Euler and the update)
+    tether_dv = (ffi.rhs(kp, x, u) - ffi.rhs(slack, x, u))[:3] * r["dt"]
+    assert np.abs((xf[:3] - xs[:3]) - tether_dv).max() < 0.05 * np.abs(tether_dv).max()
+
+
+@pytest.mark.gpu
+def test_gpu_ekf_vs_reference_expected_output(kp):
+    """The HIP EKF kernel on the reference's ekf_test inputs (tether slack, see
+    the oracle test above): within 0.01 of the MATLAB vector, and within
+    1e-12 of the oracle, for a batch of identical copies."""
+    r = _ekf_reference()
+    W, V, P0 = ok.ekf_default_covariances()
+    B = 64
+    x = np.tile(r["x_est"], (B, 1)); z = np.tile(r["measurement"], (B, 1)); u = np.zeros((B, 3))
+    P = np.repeat(P0[None], B, axis=0)
+    params = ok.load_properties()
+    params.Ks = 0.0
+    params.Kd = 0.0
+    g = ok.BatchNMPC(params, ok.default_config(), 1)
+    try:
+        xg, Pg = g.ekf_step(x, u, P, r["dt"], z, W, V)
+    finally:
+        g.close()
+    assert np.abs(xg - np.array(r["reference_est"])).max() < r["tolerance_inf"]
+    slack = kp.copy(); slack[KP_KS] = 0.0; slack[KP_KD] = 0.0
+    xo, Po = ffi.ekf_step(slack, x[0], u[0], r["dt"], P0, z[0], W, V)
+    np.testing.assert_allclose(xg, np.tile(xo, (B, 1)), rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(Pg, np.repeat(Po[None], B, axis=0), rtol=1e-11, atol=1e-13)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("update", [False, True])
 def test_gpu_ekf_vs_oracle(kp, update):

@@ -473,9 +473,128 @@ def test_kite_nmpf_facade_reference_order():
     x0 = x0_batch(1)[0]
     nm.computeControl(x0)
     U = nm.getOptimalControl(); X = nm.getOptimalTrajetory()
-    assert U.shape == (4, N) and X.shape == (15, N + 1)
+    assert U.shape == (4, N + 1) and X.shape == (15, N + 1)
+    np.testing.assert_array_equal(U[:, 0], U[:, 1])          # t = tf repeats u_{N-1}
     np.testing.assert_array_equal(X[:, -1][:13], x0[:13])
     d = nm.diagnostic()
     assert set(d) == {"pos_error", "vel_error", "cost", "virt_state", "virt_ctrl", "comp_time_ms"}
     assert nm.getStats()["return_status"] in ("Solve_Succeeded", "Maximum_Iterations_Exceeded")
     assert d["virt_state"] == X[13, -1]
+
+
+def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_frac=0.99, max_err=1e-4,
+                               max_diverged=None):
+    """B = 4096 closed loop: every step starts the GPU from the oracle's previous
+    solution (set_solution), so each step is a parity check from identical
+    inputs over the whole batch; per-kite errors relative to max(1, |oracle|)."""
+    B = 4096
+    x = x0_batch(B, offset=offset)
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    diverged = np.zeros(B, bool)
+    errs = []
+    try:
+        for step in range(steps):
+            if step > 0:
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0), nthreads=0)
+            assert not np.any(r["status"] & 1) and not np.any(st & 1)
+            same = (r["status"] & 32) == (st & 32)
+            diverged |= ~same
+            d = np.abs(r["traj"] - Xo).reshape(B, -1).max(1) / np.maximum(1.0, np.abs(Xo).reshape(B, -1).max(1))
+            c = np.abs(r["ctrl"] - Uo).reshape(B, -1).max(1) / np.maximum(1.0, np.abs(Uo).reshape(B, -1).max(1))
+            e = np.maximum(d, c)[same]
+            errs.append(e)
+            assert np.mean(e < tol) >= err_frac and e.max() < max_err, (label, step, np.sort(e)[-5:])
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+    assert diverged.sum() <= (max_diverged if max_diverged is not None else B // 1000), np.where(diverged)[0]
+    e = np.concatenate(errs)
+    print(f"{label}: B={B} x {steps} steps, {diverged.sum()} kites with differing safeguard decisions; "
+          f"kite-step errors median {np.median(e):.1e}, p99 {np.quantile(e, 0.99):.1e}, max {e.max():.1e}")
+
+
+def test_config3_full_batch_vs_oracle(kp, cfgv):
+    """BASELINE config 3 at its own size: B = 4096, N = 20, fp64, 3 closed-loop
+    steps against the oracle (same statistics as the 256-kite long loop)."""
+    _loop_vs_oracle_full_batch(kp, cfgv, ok.default_config(), 3, RTI_TOL, 9000, "config 3 fp64")
+
+
+def test_config4_fp32_sensitivities_full_batch_vs_fp64_oracle(kp, cfgv):
+    """BASELINE config 4's per-GPU slice: 4096 kites (32768 / 8 GPUs), RK4 and
+    sensitivities in fp32, condensing/QP fp64, against the fp64 oracle at the
+    fp32 RTI tolerance of SURVEY.md 8(c) (1e-4)."""
+    _loop_vs_oracle_full_batch(kp, cfgv, ok.default_config(sens_fp32=1), 3, 1e-4, 10000, "config 4 fp32-sens",
+                               max_err=1e-2)
+
+
+def test_config5_n40_fused_ekf_vs_oracle(kp):
+    """BASELINE config 5: N = 40 with the fused EKF -> RTI sequence bench.py
+    times (openkite_amd/fleet.py: 5 EKF propagation substeps of dt/5 under the
+    applied control, update with the measured position + attitude, RTI from
+    the estimate), 256 kites x 4 closed-loop steps on torch's stream.  Every
+    step, the oracle repeats the sequence from the GPU loop's own state
+    before the step (estimate, covariance, measurement, applied control, warm
+    start), so each step is a parity check from identical inputs."""
+    torch = pytest.importorskip("torch")
+    from openkite_amd.fleet import FleetLoop, GpuStepper
+    B, Nh = 256, 40
+    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    cfg = ok.default_config(N=Nh)
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    W, V, P0 = ok.ekf_default_covariances()
+    try:
+        g.set_stream(torch.cuda.current_stream().cuda_stream)
+        x0 = x0_batch(B, offset=11000)
+        loop = FleetLoop(GpuStepper(g), torch.from_numpy(x0).cuda(), Nh, cfg.dt, ekf=True, covariances=(W, V, P0))
+        for step in range(4):
+            torch.cuda.synchronize()
+            xe, P = loop.xe.cpu().numpy(), loop.P.cpu().numpy()
+            u3, z, xin = loop.u0[:, :3].cpu().numpy(), loop.z.cpu().numpy(), loop.x0.cpu().numpy()
+            Xo, Uo = g.get_solution() if step > 0 else (np.zeros((B, Nh + 1, 15)), np.zeros((B, Nh, 4)))
+            loop.step()
+            torch.cuda.synchronize()
+            for b in range(B):
+                for j in range(5):
+                    xe[b], P[b] = ffi.ekf_step(kp, xe[b], u3[b], cfg.dt / 5, P[b], z[b] if j == 4 else None, W, V)
+            np.testing.assert_allclose(loop.xe.cpu().numpy(), xe, rtol=1e-10, atol=1e-12)
+            np.testing.assert_allclose(loop.P.cpu().numpy(), P, rtol=1e-9, atol=1e-12)
+            xin[:, :13] = xe
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, xin, Xo, Uo, warm=int(step > 0), nthreads=0)
+            tr = loop.traj.cpu().numpy()
+            same = (loop.status.cpu().numpy() & 32) == (st & 32)
+            assert same.sum() >= B - 2
+            e = np.abs(tr - Xo).reshape(B, -1).max(1) / np.maximum(1.0, np.abs(Xo).reshape(B, -1).max(1))
+            e = e[same]
+            assert np.mean(e < RTI_TOL) >= 0.99 and e.max() < 1e-4, (step, np.sort(e)[-5:])
+        assert np.all(np.isfinite(loop.traj.cpu().numpy()))
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("fp32", [0, 1])
+def test_rk4_sens_hot_kernel_ragged_batch(kp, fp32):
+    """kite_nmpc_rk4_sens runs k_rk4_sens itself (the RTI's sensitivity kernel,
+    same template and launch bounds) on a ragged batch of 4099 items (8 kites
+    per block: the last block is partial), fp64 and fp32 sensitivities,
+    against the oracle.  x+ stays fp64 in both (k_defects in fp32 mode)."""
+    count = 4099
+    x = np.repeat(x0_batch(64), (count + 63) // 64, axis=0)[:count]
+    rng = np.random.default_rng(17)
+    x[:, :13] += rng.normal(scale=0.05, size=(count, 13))
+    x[:, 13:] = rng.normal(size=(count, 2))
+    u = np.column_stack([rng.uniform(0.1, 0.15, count), rng.uniform(-0.12, 0.12, (count, 2)),
+                         rng.uniform(-5, 5, count)])
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(sens_fp32=fp32), 1)
+    try:
+        xo, A, Bm = g.rk4_sens(x, u, 0.05, 2)
+    finally:
+        g.close()
+    assert np.all(np.isfinite(xo)) and np.all(np.isfinite(A)) and np.all(np.isfinite(Bm))
+    stol = 1e-4 if fp32 else 1e-10
+    for i in list(range(0, count, 41)) + list(range(count - 9, count)):
+        xr, Ar, Br = ffi.rk4_sens(kp, x[i], u[i], 0.025, 2)
+        assert rel(xo[i], xr) < 1e-12, i
+        assert rel(A[i], Ar) < stol and rel(Bm[i], Br) < stol, (i, rel(A[i], Ar), rel(Bm[i], Br))

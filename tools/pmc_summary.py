@@ -51,7 +51,13 @@ for k, d in out.items():
     d["read_bytes"] = 2.0 * d.get("FETCH_SIZE_bytes_raw", 0.0)
     d["write_bytes"] = d.get("WRITE_SIZE_bytes_raw", 0.0)
     d["traffic_bytes"] = d["read_bytes"] + d["write_bytes"]
+bench_config = None
+try:                       # the bench line of the same session: which configuration was profiled
+    bench_config = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])["run_config"]
+except Exception:
+    pass
 json.dump({"tag": tag,
+           "bench_config": bench_config,
            "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- python bench.py --steps 30 --warmup 3",
            "warmup_launches_dropped": WARMUP,
            "correction": "read = 2 x FETCH_SIZE (gfx950 coalesced-read rule), write = WRITE_SIZE; per launch",
