@@ -3,7 +3,7 @@
 Convention: FMA = 2 flops, add/mul = 1, sqrt / reciprocal / transcendental = 1.
 F_F and F_T are op counts of the device RHS template (openkite_amd/csrc/
 kite_model.hpp), produced by tools/flopcount.cpp and frozen here
-(tests/test_flops.py re-derives them).
+(tests/test_flops.py re-derives them with tools/flopcount.cpp).
 
 Per instance:
   rk4_sens : N * M * 4 * (F_F + NDIR*F_T + 4*NK*(NDIR+1))

@@ -74,3 +74,49 @@ def test_driver_matches_python_loop(tmp_path):
     # 2.65 m circle is faster than these kites can fly, so the error does not
     # vanish; scaled error 1 = 3 m)
     assert max(r["pos_error_max"] for r in steps) < 2.0
+
+
+@pytest.mark.gpu
+def test_driver_matches_oracle_closed_loop(tmp_path, kp):
+    """The driver against the CPU oracle: at every control step the oracle's RTI
+    (ffi.rti_step with the node's 0.1 s delay compensation, its own warm
+    start) from the driver's measured plant state gives the driver's u(t0)
+    and diagnostics within the RTI tolerance, and the oracle's RK4 plant
+    (4 substeps per 0.02 s simulator step, the driver's integrator) carries
+    the driver's plant state and control to the driver's next plant state."""
+    B, S, K, H = 8, 15, 3, 0.02
+    x13 = ffi.synthetic_states(B, offset=950)
+    csv = tmp_path / "x0.csv"
+    np.savetxt(csv, x13, delimiter=",", fmt="%.17g")
+    out = subprocess.run([DRIVER, "--params", PARAMS, "--batch", str(B), "--steps", str(S), "--x0", str(csv),
+                          "--ctrl-every", str(K), "--sim-dt", str(H), "--delay", "0.1", "--trace", str(B)],
+                         check=True, capture_output=True, text=True).stdout
+    recs = [json.loads(l) for l in out.strip().splitlines()]
+    diag = {(r["step"], r["kite"]): r for r in recs if r["type"] == "mpc_diagnostic"}
+    c = ffi.node_config()
+    c["delay"], c["delay_steps"] = 0.1, 4
+    cv = ffi.cfg_vector(c)
+    N = c["N"]
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    worst = 0.0
+    for s in range(S):
+        xs = np.array([diag[(s, b)]["x"] for b in range(B)])
+        x0 = np.zeros((B, 15)); x0[:, :13] = xs
+        if s == 0:
+            x0[:, 13] = [ffi.closest_point(cv, xs[b, 6:9]) for b in range(B)]
+        u0, dg, st = ffi.rti_step(kp, cv, N, 2, 16, x0, Xo, Uo, warm=int(s > 0))
+        ud = np.array([diag[(s, b)]["u"] for b in range(B)])
+        e = np.abs(ud - u0).max() / max(1.0, np.abs(u0).max())
+        worst = max(worst, e)
+        assert e < 1e-6, (s, e)
+        for b in range(B):
+            d = diag[(s, b)]
+            assert d["status"] & ~2 == st[b] & ~2
+            assert abs(d["pos_error"] - dg[b, 0]) < 1e-6 and abs(d["virt_state"] - dg[b, 3]) < 1e-6
+            if s + 1 < S:
+                x = np.zeros(15); x[:13] = d["x"]
+                u4 = np.array(d["u"]); u4[3] = 0.0
+                for _ in range(K):
+                    x = ffi.rk4(kp, x, u4, H / 4, 4); x[13:] = 0.0
+                np.testing.assert_allclose(x[:13], diag[(s + 1, b)]["x"], rtol=1e-12, atol=1e-12)
+    print(f"driver vs oracle closed loop: worst u(t0) relative difference {worst:.1e} over {S} steps")

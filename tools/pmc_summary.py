@@ -62,4 +62,38 @@ json.dump({"tag": tag,
            "warmup_launches_dropped": WARMUP,
            "correction": "read = 2 x FETCH_SIZE (gfx950 coalesced-read rule), write = WRITE_SIZE; per launch",
            "kernels": out}, open(os.path.join(prof, f"{tag}_pmc_hbm.json"), "w"), indent=1)
+# SQ pass: wave-cycle breakdown and fp64 MFMA activity per launch (steady state)
+sq_csv = os.path.join(src, "pmc_sq", "sq_counter_collection.csv")
+if os.path.exists(sq_csv):
+    per = collections.defaultdict(lambda: collections.defaultdict(dict))
+    for r in csv.DictReader(open(sq_csv)):
+        k = r["Kernel_Name"]
+        if k.startswith("k_"):
+            per[k][int(r.get("Dispatch_Id") or r.get("Correlation_Id"))][r["Counter_Name"]] = float(r["Counter_Value"])
+    sq = {}
+    SIMDS = 256 * 4
+    for k, disp in per.items():
+        ids = sorted(disp)
+        st = ids[WARMUP:] if len(ids) > WARMUP else ids
+        avg = {c: sum(disp[i].get(c, 0.0) for i in st) / len(st) for c in disp[st[0]]}
+        d = dict(avg, launches=len(st))
+        wc = avg.get("SQ_WAVE_CYCLES", 0.0)
+        if wc > 0:
+            d["frac_wait_any"] = avg.get("SQ_WAIT_ANY", 0.0) / wc
+            d["frac_wait_inst_any"] = avg.get("SQ_WAIT_INST_ANY", 0.0) / wc
+            d["frac_active_inst_any"] = avg.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
+            d["frac_active_valu"] = avg.get("SQ_ACTIVE_INST_VALU", 0.0) / wc
+        if avg.get("GRBM_GUI_ACTIVE", 0.0) > 0:
+            # MfmaUtil as rocprofv3 derives it: MFMA-busy cycles over GPU-busy cycles x SIMDs
+            d["mfma_util"] = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (avg["GRBM_GUI_ACTIVE"] * SIMDS)
+        d["mfma_f64_flops"] = avg.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) * 512.0
+        sq[k] = d
+    json.dump({"tag": tag, "bench_config": bench_config,
+               "command": "rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY "
+                          "SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 "
+                          "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- python bench.py --steps 30 --warmup 3",
+               "note": "per launch, steady-state launches; WAVE/WAIT/ACTIVE in quad-cycles summed over waves; "
+                       "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs) (rocprofv3's MfmaUtil); "
+                       "mfma_f64_flops = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512",
+               "kernels": sq}, open(os.path.join(prof, f"{tag}_sq_mfma.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
