@@ -1101,7 +1101,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                                            double* __restrict__ X, double* __restrict__ U,
                                            double* __restrict__ u0_out, double* __restrict__ diag,
                                            int32_t* __restrict__ status, double* __restrict__ kkt_out,
-                                           int32_t* __restrict__ iters_out) {
+                                           int32_t* __restrict__ iters_out,
+                                           const int32_t* __restrict__ order) {
     constexpr int NS = (NQ + 63) / 64;                 // variable slots per lane
     constexpr int NQN = (NQ - 2) / 4;                  // largest horizon
     __shared__ double Lp[NQ * (NQ + 1) / 2];
@@ -1110,7 +1111,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     __shared__ double col[NQ];
     __shared__ double dinv[NQ];
 
-    const int b = blockIdx.x;
+    const int b = order ? order[blockIdx.x] : blockIdx.x;     // longest-first dispatch (k_qp_order)
     const int l = threadIdx.x;
     const int N = C.N, n = C.n;
     const double* Hb = Hs + (size_t)b * n * n;
@@ -1592,15 +1593,42 @@ hipError_t launch_condense(const RtiConst& C, int B, const double* X, const doub
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
-                     int32_t* status, double* kkt, int32_t* iters, hipStream_t s) {
+                     int32_t* status, double* kkt, int32_t* iters, const int32_t* order, hipStream_t s) {
     if (C.n <= 82)
         hipLaunchKernelGGL(k_qp<82>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U, u0,
-                           diag, status, kkt, iters);
+                           diag, status, kkt, iters, order);
     else if (C.n <= 162)
         hipLaunchKernelGGL(k_qp<162>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U,
-                           u0, diag, status, kkt, iters);
+                           u0, diag, status, kkt, iters, order);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+// Dispatch order of the QP grid: kites by their previous step's IPM iteration
+// count, most first (a counting sort in one block; the order inside a count
+// is arbitrary and never affects a result -- every kite's QP is independent).
+// The QP waves run 4 per SIMD in sequence at B = 4096; dispatching the long
+// ones first (largest-processing-time-first list scheduling) keeps the short
+// ones for the tail, where otherwise SIMDs idle while a late long kite ends.
+__global__ __launch_bounds__(1024) void k_qp_order(int B, int K, const int32_t* __restrict__ iters,
+                                                   int32_t* __restrict__ order) {
+    __shared__ int cnt[257];
+    const int t = threadIdx.x;
+    const int nb = (K < 255 ? K : 255) + 1;
+    for (int i = t; i <= nb; i += 1024) cnt[i] = 0;
+    __syncthreads();
+    auto key = [&](int b) { const int v = iters[b]; return nb - 1 - (v < 0 ? 0 : (v > nb - 1 ? nb - 1 : v)); };
+    for (int b = t; b < B; b += 1024) atomicAdd(&cnt[key(b)], 1);
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int i = 0; i < nb; ++i) { const int c = cnt[i]; cnt[i] = acc; acc += c; }
+    }
+    __syncthreads();
+    for (int b = t; b < B; b += 1024) order[atomicAdd(&cnt[key(b)], 1)] = b;
+}
+hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, hipStream_t s) {
+    hipLaunchKernelGGL(k_qp_order, dim3(1), dim3(1024), 0, s, B, C.K, iters, order);
     return hipGetLastError();
 }
 hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,
