@@ -96,6 +96,59 @@ __device__ __forceinline__ Dual datan2(Dual y, Dual x, Dual r2) {
 }
 
 // ---------------------------------------------------------------------------
+// Dual2: value + TWO directional derivatives (k_rk4_sens, fp64): the primal
+// -- including its transcendentals -- is evaluated once for two tangent
+// directions, so 8 lanes instead of 16 cover the 16 directions of a
+// (kite, interval).
+// ---------------------------------------------------------------------------
+struct Dual2 {
+    double v, a, b;
+    Dual2() = default;
+    __host__ __device__ constexpr Dual2(double x) : v(x), a(0.0), b(0.0) {}
+    __host__ __device__ constexpr Dual2(double x, double ta, double tb) : v(x), a(ta), b(tb) {}
+};
+__device__ __forceinline__ Dual2 mk2(double v, double a, double b) { return Dual2(v, a, b); }
+__device__ __forceinline__ Dual2 operator+(Dual2 x, Dual2 y) { return mk2(x.v + y.v, x.a + y.a, x.b + y.b); }
+__device__ __forceinline__ Dual2 operator-(Dual2 x, Dual2 y) { return mk2(x.v - y.v, x.a - y.a, x.b - y.b); }
+__device__ __forceinline__ Dual2 operator-(Dual2 x) { return mk2(-x.v, -x.a, -x.b); }
+__device__ __forceinline__ Dual2 operator*(Dual2 x, Dual2 y) {
+    return mk2(x.v * y.v, fma(x.a, y.v, x.v * y.a), fma(x.b, y.v, x.v * y.b));
+}
+__device__ __forceinline__ Dual2 operator+(Dual2 x, double c) { return mk2(x.v + c, x.a, x.b); }
+__device__ __forceinline__ Dual2 operator+(double c, Dual2 x) { return mk2(x.v + c, x.a, x.b); }
+__device__ __forceinline__ Dual2 operator-(Dual2 x, double c) { return mk2(x.v - c, x.a, x.b); }
+__device__ __forceinline__ Dual2 operator-(double c, Dual2 x) { return mk2(c - x.v, -x.a, -x.b); }
+__device__ __forceinline__ Dual2 operator*(Dual2 x, double c) { return mk2(x.v * c, x.a * c, x.b * c); }
+__device__ __forceinline__ Dual2 operator*(double c, Dual2 x) { return mk2(x.v * c, x.a * c, x.b * c); }
+__device__ __forceinline__ Dual2 operator/(Dual2 x, Dual2 y) {
+    const double iy = fast_rcp(y.v);
+    const double q = x.v * iy;
+    return mk2(q, (x.a - q * y.a) * iy, (x.b - q * y.b) * iy);
+}
+__device__ __forceinline__ Dual2 operator/(Dual2 x, double c) {
+    const double ic = fast_rcp(c);
+    return mk2(x.v * ic, x.a * ic, x.b * ic);
+}
+__device__ __forceinline__ Dual2 rcp(Dual2 x) {
+    const double r = fast_rcp(x.v), nr2 = -r * r;
+    return mk2(r, x.a * nr2, x.b * nr2);
+}
+__device__ __forceinline__ double val(Dual2 x) { return x.v; }
+__device__ __forceinline__ Dual2 dsqrt(Dual2 x) {
+    const double s = sqrt(x.v), h = 0.5 * fast_rcp(s);
+    return mk2(s, x.a * h, x.b * h);
+}
+__device__ __forceinline__ Dual2 dexp(Dual2 x) { const double e = exp(x.v); return mk2(e, x.a * e, x.b * e); }
+__device__ __forceinline__ Dual2 dasin(Dual2 x, Dual2 cosv) {
+    const double ic = fast_rcp(cosv.v);
+    return mk2(asin(x.v), x.a * ic, x.b * ic);
+}
+__device__ __forceinline__ Dual2 datan2(Dual2 y, Dual2 x, Dual2 r2) {
+    const double ir = fast_rcp(r2.v);
+    return mk2(atan2(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
+}
+
+// ---------------------------------------------------------------------------
 // Single-precision dual number (mixed-precision sensitivities, config
 // sens_fp32 = 1): value and tangent in fp32 (2x the fp64 VALU rate, half the
 // registers); model constants are rounded to fp32 at use.

@@ -387,6 +387,62 @@ __global__ __launch_bounds__(RK_T, KITE_RK_OCC) void k_rk4_sens(ModelConst P, in
     }
 }
 
+// fp64 sensitivities, two tangent directions per lane (Dual2): 8 lanes per
+// (instance, interval) carry directions (2d, 2d+1) of [x_kite (13) | u_kite
+// (3)], so the primal RHS and its transcendentals run once per two tangents
+// (the 16-lane form recomputed them 16 times).  At 1 wave per SIMD the RK4
+// state (value, 2 tangents, 2 accumulator tangents) stays in registers: no
+// LDS.  Lane d writes columns 2d, 2d+1 of [A_k | B_k]; lane 0 the defect.
+constexpr int RK2_T = 64;                 // threads per block = 8 instances x 8 direction pairs
+__global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int N, int M, double h,
+                                                        const double* __restrict__ X,
+                                                        const double* __restrict__ U,
+                                                        double* __restrict__ AB, double* __restrict__ DEF) {
+    const int d = threadIdx.x & 7;
+    const int b = blockIdx.x * (RK2_T / 8) + (threadIdx.x >> 3);
+    const int k = blockIdx.y;
+    if (b >= B) return;
+    const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
+    const double* uk = U + ((size_t)b * N + k) * NU;
+    const int d0 = 2 * d, d1 = 2 * d + 1;
+    Dual2 x[NK], u[NKU];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) x[i] = Dual2(xk[i], d0 == i ? 1.0 : 0.0, d1 == i ? 1.0 : 0.0);
+#pragma unroll
+    for (int j = 0; j < NKU; ++j) u[j] = Dual2(uk[j], d0 == NK + j ? 1.0 : 0.0, d1 == NK + j ? 1.0 : 0.0);
+#pragma unroll 1
+    for (int m = 0; m < M; ++m) {
+        Dual2 xs[NK], acc[NK], kv[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
+#pragma unroll 1
+        for (int st = 0; st < 4; ++st) {
+            kite_rhs<Dual2>(P, xs, u, kv);
+            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
+            const double wn = (st < 2) ? 0.5 * h : h;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                acc[i] = Dual2(fma(wa, kv[i].v, acc[i].v), fma(wa, kv[i].a, acc[i].a), fma(wa, kv[i].b, acc[i].b));
+                xs[i] = Dual2(fma(wn, kv[i].v, x[i].v), fma(wn, kv[i].a, x[i].a), fma(wn, kv[i].b, x[i].b));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NK; ++i) x[i] = acc[i];
+    }
+    double* ab = AB + ((size_t)b * N + k) * (NK * 16);
+#pragma unroll
+    for (int i = 0; i < NK; ++i) {
+        ab[i * 16 + d0] = x[i].a;
+        ab[i * 16 + d1] = x[i].b;
+    }
+    if (d == 0) {
+        const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
+        double* df = DEF + ((size_t)b * N + k) * NK;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+    }
+}
+
 // fp64 multiple-shooting defects x+(x_k, u_k) - x_{k+1}, lane per (instance,
 // interval): the right-hand side of the QP when the sensitivities run in fp32
 __global__ __launch_bounds__(64, 2) void k_defects(ModelConst P, int B, int N, int M, double h,
@@ -1569,7 +1625,8 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
         hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF);
     }
     else
-        hipLaunchKernelGGL((k_rk4_sens<Dual, double>), grid, dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
+        hipLaunchKernelGGL(k_rk4_sens2, dim3((B + RK2_T / 8 - 1) / (RK2_T / 8), C.N), dim3(RK2_T), 0, s, P, B, C.N,
+                           C.M, C.h, X, U, AB, DEF);
     return hipGetLastError();
 }
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
