@@ -207,7 +207,7 @@ int kite_nmpc_jacobian(kite_nmpc_ctx* ctx, int32_t count, const double* x13,
  * substeps over tf: the delay-compensation predictor of nmpf_node.cpp:218.   */
 int kite_nmpc_predict(kite_nmpc_ctx* ctx, int32_t count, const double* x15,
                       const double* u4, double tf, int32_t steps, double* x15_out);
-/* The hot kernel alone (k_rk4_sens on `count` one-interval horizons, BASELINE
+/* The hot kernel alone (k_rk4_sens2 on `count` one-interval horizons, BASELINE
  * config 2): x+ and S = dx+/d[x,u] over one shooting interval (h = tf/M, M
  * substeps).  count x 15, count x 4 -> count x 15, count x 15 x 15,
  * count x 15 x 4.  Sensitivities in fp32 (x+ in fp64) when the context was

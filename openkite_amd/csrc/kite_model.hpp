@@ -11,7 +11,8 @@
 //     four half-angle sincos calls; the coefficient formulas still use the
 //     angles themselves (asin / atan2) exactly as kite.cpp:200-201;
 //   * the scalar type is a template: double for the primal, Dual (value +
-//     one tangent) for the forward sensitivities of rk4_sens.
+//     one tangent) for the Jacobian kernels, Dual2 / DualF2 (value + two
+//     tangents, fp64 / fp32) for the forward sensitivities of k_rk4_sens2.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -148,41 +149,39 @@ __device__ __forceinline__ Dual2 datan2(Dual2 y, Dual2 x, Dual2 r2) {
     return mk2(atan2(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
 }
 
-// ---------------------------------------------------------------------------
-// Single-precision dual number (mixed-precision sensitivities, config
-// sens_fp32 = 1): value and tangent in fp32 (2x the fp64 VALU rate, half the
-// registers); model constants are rounded to fp32 at use.
-// ---------------------------------------------------------------------------
-struct DualF {
-    float v, t;
-    DualF() = default;
-    __host__ __device__ constexpr DualF(double a) : v((float)a), t(0.0f) {}
-    __host__ __device__ constexpr DualF(float a, float b) : v(a), t(b) {}
+// two fp32 tangents (mixed precision, config sens_fp32 = 1, k_rk4_sens2<DualF2>)
+struct DualF2 {
+    float v, a, b;
+    DualF2() = default;
+    __host__ __device__ constexpr DualF2(double x) : v((float)x), a(0.0f), b(0.0f) {}
+    __host__ __device__ constexpr DualF2(float x, float ta, float tb) : v(x), a(ta), b(tb) {}
 };
-__device__ __forceinline__ DualF mkf(float v, float t) { return DualF(v, t); }
-__device__ __forceinline__ DualF operator+(DualF a, DualF b) { return mkf(a.v + b.v, a.t + b.t); }
-__device__ __forceinline__ DualF operator-(DualF a, DualF b) { return mkf(a.v - b.v, a.t - b.t); }
-__device__ __forceinline__ DualF operator-(DualF a) { return mkf(-a.v, -a.t); }
-__device__ __forceinline__ DualF operator*(DualF a, DualF b) { return mkf(a.v * b.v, fmaf(a.t, b.v, a.v * b.t)); }
-__device__ __forceinline__ DualF operator+(DualF a, double b) { return mkf(a.v + (float)b, a.t); }
-__device__ __forceinline__ DualF operator+(double b, DualF a) { return mkf(a.v + (float)b, a.t); }
-__device__ __forceinline__ DualF operator-(DualF a, double b) { return mkf(a.v - (float)b, a.t); }
-__device__ __forceinline__ DualF operator-(double b, DualF a) { return mkf((float)b - a.v, -a.t); }
-__device__ __forceinline__ DualF operator*(DualF a, double b) { const float f = (float)b; return mkf(a.v * f, a.t * f); }
-__device__ __forceinline__ DualF operator*(double b, DualF a) { const float f = (float)b; return mkf(a.v * f, a.t * f); }
-__device__ __forceinline__ DualF operator/(DualF a, DualF b) {
-    const float ib = 1.0f / b.v;
-    const float q = a.v * ib;
-    return mkf(q, (a.t - q * b.t) * ib);
+__device__ __forceinline__ DualF2 mkf2(float v, float a, float b) { return DualF2(v, a, b); }
+__device__ __forceinline__ DualF2 operator+(DualF2 x, DualF2 y) { return mkf2(x.v + y.v, x.a + y.a, x.b + y.b); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x, DualF2 y) { return mkf2(x.v - y.v, x.a - y.a, x.b - y.b); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x) { return mkf2(-x.v, -x.a, -x.b); }
+__device__ __forceinline__ DualF2 operator*(DualF2 x, DualF2 y) {
+    return mkf2(x.v * y.v, fmaf(x.a, y.v, x.v * y.a), fmaf(x.b, y.v, x.v * y.b));
 }
-__device__ __forceinline__ DualF operator/(DualF a, double b) { const float ib = (float)(1.0 / b); return mkf(a.v * ib, a.t * ib); }
-__device__ __forceinline__ DualF rcp(DualF a) { const float r = 1.0f / a.v; return mkf(r, -a.t * r * r); }
-__device__ __forceinline__ float val(DualF a) { return a.v; }
-__device__ __forceinline__ DualF dsqrt(DualF a) { const float s = sqrtf(a.v); return mkf(s, a.t * (0.5f / s)); }
-__device__ __forceinline__ DualF dexp(DualF a) { const float e = expf(a.v); return mkf(e, a.t * e); }
-__device__ __forceinline__ DualF dasin(DualF x, DualF cosv) { return mkf(asinf(x.v), x.t / cosv.v); }
-__device__ __forceinline__ DualF datan2(DualF y, DualF x, DualF r2) {
-    return mkf(atan2f(y.v, x.v), (x.v * y.t - y.v * x.t) / r2.v);
+__device__ __forceinline__ DualF2 operator+(DualF2 x, double c) { return mkf2(x.v + (float)c, x.a, x.b); }
+__device__ __forceinline__ DualF2 operator+(double c, DualF2 x) { return mkf2(x.v + (float)c, x.a, x.b); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x, double c) { return mkf2(x.v - (float)c, x.a, x.b); }
+__device__ __forceinline__ DualF2 operator-(double c, DualF2 x) { return mkf2((float)c - x.v, -x.a, -x.b); }
+__device__ __forceinline__ DualF2 operator*(DualF2 x, double c) { const float f = (float)c; return mkf2(x.v * f, x.a * f, x.b * f); }
+__device__ __forceinline__ DualF2 operator*(double c, DualF2 x) { const float f = (float)c; return mkf2(x.v * f, x.a * f, x.b * f); }
+__device__ __forceinline__ DualF2 operator/(DualF2 x, DualF2 y) {
+    const float iy = 1.0f / y.v, q = x.v * iy;
+    return mkf2(q, (x.a - q * y.a) * iy, (x.b - q * y.b) * iy);
+}
+__device__ __forceinline__ DualF2 operator/(DualF2 x, double c) { const float ic = (float)(1.0 / c); return mkf2(x.v * ic, x.a * ic, x.b * ic); }
+__device__ __forceinline__ DualF2 rcp(DualF2 x) { const float r = 1.0f / x.v, nr2 = -r * r; return mkf2(r, x.a * nr2, x.b * nr2); }
+__device__ __forceinline__ float val(DualF2 x) { return x.v; }
+__device__ __forceinline__ DualF2 dsqrt(DualF2 x) { const float s = sqrtf(x.v), h = 0.5f / s; return mkf2(s, x.a * h, x.b * h); }
+__device__ __forceinline__ DualF2 dexp(DualF2 x) { const float e = expf(x.v); return mkf2(e, x.a * e, x.b * e); }
+__device__ __forceinline__ DualF2 dasin(DualF2 x, DualF2 cosv) { const float ic = 1.0f / cosv.v; return mkf2(asinf(x.v), x.a * ic, x.b * ic); }
+__device__ __forceinline__ DualF2 datan2(DualF2 y, DualF2 x, DualF2 r2) {
+    const float ir = 1.0f / r2.v;
+    return mkf2(atan2f(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
 }
 
 template <class T> struct V3 { T x, y, z; };

@@ -1,6 +1,6 @@
 // rti_kernels.hip -- batched RTI step for the openKITE kite NMPC on gfx950.
 //
-// One RTI step = k_prologue -> k_rk4_sens -> k_condense -> k_qp (see
+// One RTI step = k_prologue -> k_rk4_sens2 -> k_condense -> k_qp (see
 // DESIGN.md).  Replaces KiteNMPF::computeControl's NLP_Solver(ARG) call
 // (src/kite_control/kiteNMPF.cpp:199-316).
 //
@@ -300,93 +300,12 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
 }
 
 // ---------------------------------------------------------------------------
-// k_rk4_sens: the hot kernel.  One lane per (instance, interval, direction);
-// a wavefront covers one shooting interval of 4 instances x 16 directions
-// (13 kite states + 3 kite controls; theta/thetadot/Uv are an exact double
-// integrator and are handled analytically in k_condense).  Each lane carries
-// value + tangent through M RK4 substeps (kitemath.cpp:36-51) and writes one
-// column of [A_k | B_k]; lane 0 of each instance writes the defect.
+// k_rk4_sens2: the sensitivity kernel.  RK4 (kitemath.cpp:36-51) with M
+// substeps of the 13-state kite ODE under constant u_k, carried with forward
+// tangents in the 16 directions [x_kite (13) | u_kite (3)] -> [A_k | B_k] and
+// the defect x+ - x_{k+1}; theta/thetadot/Uv (an exact double integrator) are
+// handled analytically in k_condense.
 // ---------------------------------------------------------------------------
-// Classic RK4 (M substeps) on value + one tangent.  One dual RHS needs ~166
-// VGPRs; the substep start state x (value+tangent) and the tangent half of
-// the accumulator live in LDS (SoA [component][lane], conflict-free,
-// 312 B/lane, 39 KiB per 128-lane block).  Occupancy: KITE_RK_OCC = 1 wave
-// per SIMD (512 registers): at 2 waves/SIMD the kernel spilled 160 B/lane to
-// scratch (same speed, 0.25 GB more HBM traffic per launch).
-constexpr int RK_T = 128;                 // threads per rk4 block = 8 instances x 16 dirs
-#ifndef KITE_RK_OCC
-#define KITE_RK_OCC 1                     // launch_bounds occupancy hint of k_rk4_sens (1: 512 regs, no scratch spill)
-#endif
-constexpr int RK_LDS = 3 * NK;            // x.v, x.t, acc.t
-// DT: dual number (Dual fp64 / DualF fp32 for config.sens_fp32), ST: its scalar
-template <class DT, class ST>
-__device__ __forceinline__ void rk4_dual(const ModelConst& P, DT* x /*in/out [NK]*/, const DT* u, ST h, int M,
-                                         ST (*sh)[RK_T], int tid) {
-    for (int m = 0; m < M; ++m) {
-        DT xs[NK], kv[NK];
-        ST accv[NK];
-#pragma unroll
-        for (int i = 0; i < NK; ++i) {
-            sh[i][tid] = x[i].v;
-            sh[NK + i][tid] = x[i].t;
-            sh[2 * NK + i][tid] = x[i].t;
-            xs[i] = x[i];
-            accv[i] = x[i].v;
-        }
-        // keep the compiler from forwarding the LDS stores back into registers
-        asm volatile("" ::: "memory");
-#pragma unroll 1
-        for (int st = 0; st < 4; ++st) {
-            kite_rhs<DT>(P, xs, u, kv);
-            const ST wa = (st == 0 || st == 3) ? h / ST(6) : h / ST(3);
-            const ST wn = (st < 2) ? ST(0.5) * h : h;
-#pragma unroll
-            for (int i = 0; i < NK; ++i) {
-                accv[i] = fma(wa, kv[i].v, accv[i]);
-                sh[2 * NK + i][tid] = fma(wa, kv[i].t, sh[2 * NK + i][tid]);
-                xs[i] = DT(fma(wn, kv[i].v, sh[i][tid]), fma(wn, kv[i].t, sh[NK + i][tid]));
-            }
-            asm volatile("" ::: "memory");
-        }
-#pragma unroll
-        for (int i = 0; i < NK; ++i) x[i] = DT(accv[i], sh[2 * NK + i][tid]);
-    }
-}
-
-template <class DT, class ST>
-__global__ __launch_bounds__(RK_T, KITE_RK_OCC) void k_rk4_sens(ModelConst P, int B, int N, int M, double h,
-                                                             const double* __restrict__ X,
-                                                             const double* __restrict__ U,
-                                                             double* __restrict__ AB,
-                                                             double* __restrict__ DEF) {
-    __shared__ ST xsh[RK_LDS][RK_T];
-    const int d = threadIdx.x & 15;
-    const int b = blockIdx.x * (RK_T / 16) + (threadIdx.x >> 4);
-    const int k = blockIdx.y;
-    if (b >= B) return;
-    const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
-    const double* uk = U + ((size_t)b * N + k) * NU;
-    DT x[NK], u[NKU];
-#pragma unroll
-    for (int i = 0; i < NK; ++i) x[i] = DT(ST(xk[i]), ST(d == i ? 1 : 0));
-#pragma unroll
-    for (int j = 0; j < NKU; ++j) u[j] = DT(ST(uk[j]), ST(d == NK + j ? 1 : 0));
-    rk4_dual<DT, ST>(P, x, u, ST(h), M, xsh, threadIdx.x);
-    double* ab = AB + ((size_t)b * N + k) * (NK * 16);
-#pragma unroll
-    for (int i = 0; i < NK; ++i) ab[i * 16 + d] = (double)x[i].t;
-    if (d == 0) {
-        const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
-        double* df = DEF + ((size_t)b * N + k) * NK;
-        // mixed precision: the defects (the QP's right-hand side) come from
-        // the fp64 primal of k_defects; only the sensitivities are fp32 here
-        if constexpr (std::is_same<ST, double>::value) {
-#pragma unroll
-            for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
-        }
-    }
-}
-
 // fp64 sensitivities, two tangent directions per lane (Dual2): 8 lanes per
 // (instance, interval) carry directions (2d, 2d+1) of [x_kite (13) | u_kite
 // (3)], so the primal RHS and its transcendentals run once per two tangents
@@ -394,6 +313,9 @@ __global__ __launch_bounds__(RK_T, KITE_RK_OCC) void k_rk4_sens(ModelConst P, in
 // state (value, 2 tangents, 2 accumulator tangents) stays in registers: no
 // LDS.  Lane d writes columns 2d, 2d+1 of [A_k | B_k]; lane 0 the defect.
 constexpr int RK2_T = 64;                 // threads per block = 8 instances x 8 direction pairs
+// DT: Dual2 (fp64) or DualF2 (fp32 sensitivities, config sens_fp32 = 1; the
+// defects then come from k_defects in fp64), ST its scalar
+template <class DT, class ST>
 __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int N, int M, double h,
                                                         const double* __restrict__ X,
                                                         const double* __restrict__ U,
@@ -405,25 +327,26 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
     const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
     const double* uk = U + ((size_t)b * N + k) * NU;
     const int d0 = 2 * d, d1 = 2 * d + 1;
-    Dual2 x[NK], u[NKU];
+    const ST one = ST(1), zero = ST(0), hs = ST(h);
+    DT x[NK], u[NKU];
 #pragma unroll
-    for (int i = 0; i < NK; ++i) x[i] = Dual2(xk[i], d0 == i ? 1.0 : 0.0, d1 == i ? 1.0 : 0.0);
+    for (int i = 0; i < NK; ++i) x[i] = DT(ST(xk[i]), d0 == i ? one : zero, d1 == i ? one : zero);
 #pragma unroll
-    for (int j = 0; j < NKU; ++j) u[j] = Dual2(uk[j], d0 == NK + j ? 1.0 : 0.0, d1 == NK + j ? 1.0 : 0.0);
+    for (int j = 0; j < NKU; ++j) u[j] = DT(ST(uk[j]), d0 == NK + j ? one : zero, d1 == NK + j ? one : zero);
 #pragma unroll 1
     for (int m = 0; m < M; ++m) {
-        Dual2 xs[NK], acc[NK], kv[NK];
+        DT xs[NK], acc[NK], kv[NK];
 #pragma unroll
         for (int i = 0; i < NK; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
 #pragma unroll 1
         for (int st = 0; st < 4; ++st) {
-            kite_rhs<Dual2>(P, xs, u, kv);
-            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
-            const double wn = (st < 2) ? 0.5 * h : h;
+            kite_rhs<DT>(P, xs, u, kv);
+            const ST wa = (st == 0 || st == 3) ? hs / ST(6) : hs / ST(3);
+            const ST wn = (st < 2) ? ST(0.5) * hs : hs;
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
-                acc[i] = Dual2(fma(wa, kv[i].v, acc[i].v), fma(wa, kv[i].a, acc[i].a), fma(wa, kv[i].b, acc[i].b));
-                xs[i] = Dual2(fma(wn, kv[i].v, x[i].v), fma(wn, kv[i].a, x[i].a), fma(wn, kv[i].b, x[i].b));
+                acc[i] = DT(fma(wa, kv[i].v, acc[i].v), fma(wa, kv[i].a, acc[i].a), fma(wa, kv[i].b, acc[i].b));
+                xs[i] = DT(fma(wn, kv[i].v, x[i].v), fma(wn, kv[i].a, x[i].a), fma(wn, kv[i].b, x[i].b));
             }
         }
 #pragma unroll
@@ -432,14 +355,16 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
     double* ab = AB + ((size_t)b * N + k) * (NK * 16);
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
-        ab[i * 16 + d0] = x[i].a;
-        ab[i * 16 + d1] = x[i].b;
+        ab[i * 16 + d0] = (double)x[i].a;
+        ab[i * 16 + d1] = (double)x[i].b;
     }
-    if (d == 0) {
-        const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
-        double* df = DEF + ((size_t)b * N + k) * NK;
+    if constexpr (std::is_same<ST, double>::value) {
+        if (d == 0) {
+            const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
+            double* df = DEF + ((size_t)b * N + k) * NK;
 #pragma unroll
-        for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+            for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+        }
     }
 }
 
@@ -1554,7 +1479,7 @@ __global__ __launch_bounds__(64, 2) void k_predict(ModelConst P, int count, cons
 }
 
 // rk4 with sensitivities for independent (x,u) items (API kite_nmpc_rk4_sens):
-// the items run through the hot kernel k_rk4_sens itself as a batch of
+// the items run through the hot kernel k_rk4_sens2 itself as a batch of
 // one-interval horizons (N = 1, node 1 = 0 so the "defect" is x+), then
 // k_sens_items_expand writes the full 15x15 / 15x4 blocks with the exact
 // theta/thetadot/Uv rows and columns.  X2 [count][2][15] is scratch.
@@ -1619,14 +1544,15 @@ hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int wa
 }
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
                            double* AB, double* DEF, hipStream_t s) {
-    const dim3 grid((B + RK_T / 16 - 1) / (RK_T / 16), C.N);
+    const dim3 grid2((B + RK2_T / 8 - 1) / (RK2_T / 8), C.N);
     if (C.sens_fp32) {
-        hipLaunchKernelGGL((k_rk4_sens<DualF, float>), grid, dim3(RK_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB, DEF);
+        hipLaunchKernelGGL((k_rk4_sens2<DualF2, float>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB,
+                           DEF);
         hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF);
+    } else {
+        hipLaunchKernelGGL((k_rk4_sens2<Dual2, double>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB,
+                           DEF);
     }
-    else
-        hipLaunchKernelGGL(k_rk4_sens2, dim3((B + RK2_T / 8 - 1) / (RK2_T / 8), C.N), dim3(RK2_T), 0, s, P, B, C.N,
-                           C.M, C.h, X, U, AB, DEF);
     return hipGetLastError();
 }
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,

@@ -32,7 +32,7 @@ struct RtiConst {
     double path_R, path_alt, pq[4];
     double delay;       // delay compensation [s] (0 = off)
     int delay_steps, delay_node;
-    int sens_fp32, pad2_;   // 1: k_rk4_sens in fp32 (DualF)
+    int sens_fp32, pad2_;   // 1: k_rk4_sens2 in fp32 (DualF2)
 };
 
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,

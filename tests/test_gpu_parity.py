@@ -576,7 +576,7 @@ def test_config5_n40_fused_ekf_vs_oracle(kp):
 
 @pytest.mark.parametrize("fp32", [0, 1])
 def test_rk4_sens_hot_kernel_ragged_batch(kp, fp32):
-    """kite_nmpc_rk4_sens runs k_rk4_sens itself (the RTI's sensitivity kernel,
+    """kite_nmpc_rk4_sens runs k_rk4_sens2 itself (the RTI's sensitivity kernel,
     same template and launch bounds) on a ragged batch of 4099 items (8 kites
     per block: the last block is partial), fp64 and fp32 sensitivities,
     against the oracle.  x+ stays fp64 in both (k_defects in fp32 mode)."""
