@@ -39,6 +39,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     hi = __builtin_amdgcn_readlane(hi, lane);
     return __hiloint2double(hi, lo);
 }
+// LDS exchange between the lanes of ONE wavefront: a wavefront-scope fence
+// pair around the wave barrier (no s_barrier; used where a block is a single
+// wave, or where one wave of a block works alone)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 // ---------------------------------------------------------------------------
 // cross-lane primitives, all VALU (no LDS round trip).  Lane semantics of the
 // gfx950 permlane swaps, probed on the device (tools/probes/lane_ops.hip):
@@ -844,6 +852,297 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// k_condense20: N = 20 condensing for the tiled QP, ONE wavefront per kite.
+// Same algebra as k_condense, organised for latency: every node's 4 residual
+// rows (3 path rows, 1 path-speed row; Mayer rows at node N) ARE one k-step
+// of v_mfma_f64_16x16x4_f64, so each node is folded into H_aa as soon as its
+// rows exist (15 lower 16x16 tiles = 60 accumulators per lane) -- no 16-row
+// chunk buffer, no second wave, no block barrier (wavefront fences only).
+// The three columns past the control block (theta0, thetadot0 and the
+// affine residual column that yields the gradient) are accumulated on the
+// VALU against variable i = l (slot 0) and 64 + l (slot 1): H_ab, H_bb and h
+// come straight out of them.  Small footprint (~14 KB LDS) so two kites share
+// a SIMD (launch bound 2 waves / SIMD).
+//   lane t < 60 : column t of G (kite control (k = t/3, c = t%3)), 13 rows in VGPRs
+//   lane 60     : the affine column g (propagated defects)
+// ---------------------------------------------------------------------------
+constexpr int CD20_N = 20, CD20_NA = 80, CD20_n = 82;
+constexpr int CD20_WLD = 112;                    // Wc row stride: 2*WLD % 64 == 32 -> conflict-free tile reads
+__global__ __launch_bounds__(64, 2) void k_condense20(RtiConst C, int B, const double* __restrict__ X,
+                                                      const double* __restrict__ U,
+                                                      const double* __restrict__ AB,
+                                                      const double* __restrict__ DEF, double* __restrict__ hs,
+                                                      double* __restrict__ Cr, double* __restrict__ cl,
+                                                      double* __restrict__ cu, double* __restrict__ hmax,
+                                                      double* __restrict__ Htl, double* __restrict__ Hab,
+                                                      double* __restrict__ Hbb) {
+    constexpr int N = CD20_N, n = CD20_n, NA = CD20_NA, WLD = CD20_WLD;
+    constexpr int SAL = 16 * 16 + NK + 3;
+    __shared__ double sA[2][SAL];                    // [A_k | B_k] column-major (col j: 16 j + i), then d_k
+    __shared__ double Wc[4 * WLD];                   // the 4 residual rows of the current node
+    __shared__ double sX[(N + 1) * NX];
+    __shared__ double sPth[N + 1][6];
+    __shared__ double sScl[96], sRd[96], sRu[96];
+    __shared__ double sHx[3][96];
+    const int b = blockIdx.x;
+    const int l = threadIdx.x;
+    if (b >= B) return;
+    const double* Xb = X + (size_t)b * (N + 1) * NX;
+    const double* Ub = U + (size_t)b * N * NU;
+    const double* ABb = AB + (size_t)b * N * NK * 16;
+    const double* DEFb = DEF + (size_t)b * N * NK;
+
+    {   // trajectory up front (all loads in flight first), path per node, scale tables
+        constexpr int NXL = ((N + 1) * NX + 63) / 64;
+        double xv[NXL];
+#pragma unroll
+        for (int q = 0; q < NXL; ++q) {
+            const int i = l + 64 * q;
+            xv[q] = i < (N + 1) * NX ? Xb[i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NXL; ++q) {
+            const int i = l + 64 * q;
+            if (i < (N + 1) * NX) sX[i] = xv[q];
+        }
+    }
+    if (l <= N) {
+        double Pp[3], dP[3];
+        path_eval(C, Xb[l * NX + 13], Pp, dP);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { sPth[l][a] = Pp[a]; sPth[l][3 + a] = dP[a]; }
+    }
+    {
+        const double iS0 = 1.0 / C.Su[0], iS1 = 1.0 / C.Su[1], iS2 = 1.0 / C.Su[2], iS3 = 1.0 / C.Su[3];
+        const double R0 = C.Rdiag[0], R1 = C.Rdiag[1], R2 = C.Rdiag[2], R3 = C.Rdiag[3];
+        for (int i = l; i < 96; i += 64) {
+            double sc = 0.0, rd = 0.0, ub = 0.0;
+            if (i < 3 * N) {
+                const int c = i % 3;
+                sc = c == 0 ? iS0 : (c == 1 ? iS1 : iS2);
+                rd = c == 0 ? R0 : (c == 1 ? R1 : R2);
+                ub = Ub[(i / 3) * NU + c];
+            } else if (i < 4 * N) {
+                sc = iS3; rd = R3; ub = Ub[(i - 3 * N) * NU + 3];
+            } else if (i == 4 * N) {
+                sc = 1.0 / C.Sx13;
+            } else if (i == 4 * N + 1) {
+                sc = 1.0 / C.Sx14;
+            }
+            sScl[i] = sc; sRd[i] = rd; sRu[i] = rd * ub;
+        }
+    }
+    const bool kite_lane = l < 3 * N;
+    const bool aff_lane = (l == 3 * N);
+    const int kb = l / 3, cc = l % 3;
+    // select by value: a lane-dependent index into the kernel-argument struct
+    // would copy the struct to scratch
+    const double Dl = kite_lane ? 1.0 / (cc == 0 ? C.Su[0] : (cc == 1 ? C.Su[1] : C.Su[2])) : 0.0;
+    double v[NK];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) v[i] = 0.0;
+    double4v acc[QP_NTILE];
+#pragma unroll
+    for (int q = 0; q < QP_NTILE; ++q) acc[q] = double4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {                    // H_ext[i][80 + c], i < 83
+        sHx[c][l] = 0.0;
+        if (l < 96 - 64) sHx[c][64 + l] = 0.0;
+    }
+
+    // interval data PD nodes ahead in a register ring (221 doubles -> 4 per lane)
+    constexpr int NPF = (NK * 16 + NK + 63) / 64;
+    constexpr int PD = 1;
+    double pf[PD][NPF];
+    auto load_iv = [&](int k, double* dst) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < NPF; ++q) {
+            const int e = l + 64 * q;
+            double val = 0.0;
+            if (e < NK * 16) val = ABb[(size_t)k * NK * 16 + e];
+            else if (e < NK * 16 + NK) val = DEFb[(size_t)k * NK + (e - NK * 16)];
+            dst[q] = val;
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < PD; ++q) load_iv(q, pf[q]);
+    double wpD[3], wpT[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { wpD[a] = C.sqQ_dt[a] * C.Sr[a]; wpT[a] = C.sqQ_T[a] * C.Sr[a]; }
+    double* Crb = Cr + (size_t)b * N * n;
+
+    auto node = [&](int k, double* pfs) __attribute__((always_inline)) {
+        const bool last = (k == N);
+        const int par = k & 1;
+        if (!last) {
+#pragma unroll
+            for (int q = 0; q < NPF; ++q) {
+                const int e = l + 64 * q;
+                if (e < NK * 16) sA[par][(e & 15) * 16 + (e >> 4)] = pfs[q];       // transpose: column-major
+                else if (e < NK * 16 + NK) sA[par][16 * 16 + (e - NK * 16)] = pfs[q];
+            }
+        }
+        wave_sync();                  // sA[par] visible; the previous node's Wc reads are done
+        if (k + PD < N) load_iv(k + PD, pfs);
+        // the affine column at node k, wave-uniform (lane 60)
+        const double g0 = uniform_d(readlane_d(v[0], 3 * N));
+        const double gr0 = uniform_d(readlane_d(v[6], 3 * N));
+        const double gr1 = uniform_d(readlane_d(v[7], 3 * N));
+        const double gr2 = uniform_d(readlane_d(v[8], 3 * N));
+        const double gr[3] = {gr0, gr1, gr2};
+        const double* xk = sX + k * NX;
+        const double thd = xk[14];
+        double wp[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) wp[a] = last ? wpT[a] : wpD[a];
+        const double wv = last ? 0.0 : C.sw * C.sv;
+        // residual rows of node k: kite columns (path rows -sq sr G[6+a], speed row 0)
+        if (kite_lane) {
+            Wc[0 * WLD + l] = -wp[0] * v[6];
+            Wc[1 * WLD + l] = -wp[1] * v[7];
+            Wc[2 * WLD + l] = -wp[2] * v[8];
+            Wc[3 * WLD + l] = 0.0;
+        }
+        // analytic columns 3N .. n (Uv_m, theta0, thetadot0, affine)
+        if (l < N + 3) {
+            const int col = 3 * N + l;
+            double cth = 0.0, cthd = 0.0;
+            if (l < N) {
+                if (k > l) { cth = C.dt * C.dt * ((double)(k - l) - 0.5); cthd = C.dt; }
+            } else if (l == N) {
+                cth = 1.0;
+            } else if (l == N + 1) {
+                cth = (double)k * C.dt; cthd = 1.0;
+            }
+            if (l < N + 2) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) Wc[a * WLD + col] = wp[a] * sPth[k][3 + a] * cth;
+                Wc[3 * WLD + col] = -wv * cthd;
+            } else {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) Wc[a * WLD + col] = wp[a] * (sPth[k][a] - xk[6 + a] - gr[a]);
+                Wc[3 * WLD + col] = last ? 0.0 : C.sw * (C.sv * C.vref - C.sv * thd);
+            }
+        }
+        // vx bound row of node k >= 1 (kite-control columns; the rest zero)
+        if (k >= 1) {
+            double* crow = Crb + (size_t)(k - 1) * n;
+            crow[l] = kite_lane ? v[0] * Dl : 0.0;
+            if (l < n - 64) crow[64 + l] = 0.0;
+            if (l == 0) {
+                const double base = xk[0] + g0;
+                cl[(size_t)b * N + k - 1] = C.lo_fin ? (C.lbx[0] - base) : -INFINITY;
+                cu[(size_t)b * N + k - 1] = C.hi_fin ? (C.ubx[0] - base) : INFINITY;
+            }
+        }
+        wave_sync();
+        // fold: the node's 4 rows are one MFMA k-step of H_aa += W_k' W_k
+        {
+            double fr[QP_NTA];
+#pragma unroll
+            for (int I = 0; I < QP_NTA; ++I) fr[I] = Wc[(l >> 4) * WLD + 16 * I + (l & 15)];
+#pragma unroll
+            for (int I = 0; I < QP_NTA; ++I)
+#pragma unroll
+                for (int J = 0; J <= I; ++J)
+                    acc[I * (I + 1) / 2 + J] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[I], fr[J], acc[I * (I + 1) / 2 + J], 0, 0, 0);
+        }
+        // the columns past the control block against rows i = l, 64 + l,
+        // accumulated in LDS (sHx[c][i]: no long-lived registers)
+        {
+            double t0[3] = {0.0, 0.0, 0.0}, t1[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double w0 = Wc[r * WLD + l];
+                const double w1 = l < n + 1 - 64 ? Wc[r * WLD + 64 + l] : 0.0;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const double we = Wc[r * WLD + NA + c];
+                    t0[c] = fma(w0, we, t0[c]);
+                    t1[c] = fma(w1, we, t1[c]);
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                sHx[c][l] += t0[c];
+                if (l < n + 1 - 64) sHx[c][64 + l] += t1[c];
+            }
+        }
+        if (!last) {
+            // G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
+            const double* sa = sA[par];
+            if ((kite_lane && k >= kb) || aff_lane) {
+                double nv[NK];
+                if (kite_lane && k == kb) {
+#pragma unroll
+                    for (int i = 0; i < NK; ++i) nv[i] = sa[(NK + cc) * 16 + i];
+                } else {
+                    const double am = aff_lane ? 1.0 : 0.0;
+#pragma unroll
+                    for (int i = 0; i < NK; ++i) nv[i] = am * sa[16 * 16 + i];
+                    // column-oriented, one column of A_k in registers at a
+                    // time (the memory clobber keeps the compiler from
+                    // hoisting all 169 LDS loads into registers)
+#pragma unroll
+                    for (int j = 0; j < NK; ++j) {
+                        double ac[NK];
+#pragma unroll
+                        for (int i = 0; i < NK; ++i) ac[i] = sa[j * 16 + i];
+                        const double vj = v[j];
+#pragma unroll
+                        for (int i = 0; i < NK; ++i) nv[i] = fma(ac[i], vj, nv[i]);
+                        asm volatile("" ::: "memory");
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NK; ++i) v[i] = nv[i];
+            }
+        }
+    };
+#pragma unroll 1
+    for (int k = 0; k <= N; ++k) node(k, pf[0]);
+
+    // scaled QP out: H_aa tiles (+ R diagonal) in the tiled QP's lane order,
+    // H_ab / H_bb / h from the three extra columns; hmax = max |H|
+    double lmax = 0.0;
+#pragma unroll
+    for (int I = 0; I < QP_NTA; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+            const int t = I * (I + 1) / 2 + J;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = 16 * I + (l >> 4) + 4 * r, gj = 16 * J + (l & 15);
+                double hv = acc[t][r];
+                if (gi == gj) hv += sRd[gi];
+                hv *= sScl[gi] * sScl[gj];
+                Htl[((size_t)b * QP_NTILE + t) * 256 + r * 64 + l] = hv;
+                lmax = fmax(lmax, fabs(hv));
+            }
+        }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int i = l + 64 * s2;
+        const double hxa = i < 96 ? sHx[0][i] : 0.0, hxb = i < 96 ? sHx[1][i] : 0.0;
+        const double hxc = i < 96 ? sHx[2][i] : 0.0;
+        if (i < NA) {
+            const double a0 = hxa * sScl[i] * sScl[NA], a1 = hxb * sScl[i] * sScl[NA + 1];
+            Hab[((size_t)b * NA + i) * 2 + 0] = a0;
+            Hab[((size_t)b * NA + i) * 2 + 1] = a1;
+            lmax = fmax(lmax, fmax(fabs(a0), fabs(a1)));
+        } else if (i < n) {
+            const double a0 = hxa * sScl[i] * sScl[NA], a1 = hxb * sScl[i] * sScl[NA + 1];
+            Hbb[(size_t)b * 4 + (i - NA) * 2 + 0] = a0;
+            Hbb[(size_t)b * 4 + (i - NA) * 2 + 1] = a1;
+            lmax = fmax(lmax, fmax(fabs(a0), fabs(a1)));
+        }
+        if (i < n) hs[(size_t)b * n + i] = (hxc + sRu[i]) * sScl[i];
+    }
+    lmax = wave_max(lmax);
+    if (l == 0) hmax[b] = lmax;
+}
+
 #ifdef KITE_QP_PROF
 // tools only: read and clear the condensing phase profile (8 x uint64)
 extern "C" int kite_debug_cd_profile(unsigned long long* out) {
@@ -868,11 +1167,6 @@ extern "C" int kite_debug_cd_profile(unsigned long long* out) {
 // wavefront; w = scaled QP step in slots (i = l + 64 s); vec/col: LDS scratch.
 // WAVE: the caller is one wavefront of a larger block (the other waves have
 // left), so the LDS exchanges are ordered by a wavefront fence, not s_barrier.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 template <int NS, bool WAVE = false>
 __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[NS], double kkt, int iters,
                              const double* __restrict__ AB, const double* __restrict__ DEF,
@@ -1558,6 +1852,11 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
                            const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
                            double* hmax, int tiled, double* Htl, double* Hab, double* Hbb, hipStream_t s) {
+    if (tiled && C.N == CD20_N && C.n == CD20_n) {
+        hipLaunchKernelGGL(k_condense20, dim3(B), dim3(64), 0, s, C, B, X, U, AB, DEF, hs, Cr, cl, cu, hmax, Htl,
+                           Hab, Hbb);
+        return hipGetLastError();
+    }
     const int NR = (C.n + 1 + 15) / 16;
 #define KITE_CONDENSE(R)                                                                                    \
     case R:                                                                                                 \
