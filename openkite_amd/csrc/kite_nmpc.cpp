@@ -39,7 +39,8 @@ struct kite_nmpc_ctx {
     double *u0 = nullptr, *diag = nullptr, *kkt = nullptr;
     int32_t* status = nullptr;
     int32_t* iters = nullptr;
-    int32_t* order = nullptr;      // QP dispatch order (k_qp_order), B entries
+    int32_t* order = nullptr;      // QP dispatch order (k_qp_order), B entries, then the lazy
+                                   // state-bound list (B + 1: count, kites)
     // tiled-QP layout (N == 20, 40): H_aa lower tiles [B][NT(NT+1)/2][4][64] with
     // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
@@ -197,16 +198,16 @@ int run_step(kite_nmpc_ctx* ctx) {
                                   ctx->cl, ctx->cu, ctx->hmax, ctx->tiled ? 1 : 0, ctx->Htl, ctx->Hab, ctx->Hbb,
                                   s));
     // QP dispatch order from the previous step's iteration counts (ctx->iters[0, B))
-    HIP_TRY(kite::launch_qp_order(ctx->rc, B, ctx->iters, ctx->order, s));
+    HIP_TRY(kite::launch_qp_order(ctx->rc, B, ctx->iters, ctx->order, ctx->order + B, s));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
     if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
                                       ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
-                                      ctx->status, ctx->kkt, ctx->iters, ctx->order, s));
+                                      ctx->status, ctx->kkt, ctx->iters, ctx->order, ctx->order + B, s));
     else
         HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
                                 ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters,
-                                ctx->order, s));
+                                ctx->order, ctx->order + B, s));
     if (ev) HIP_TRY(hipEventRecord(ev[4], s));
     ctx->timed_step = (ev == ctx->ev);
     ctx->warm = true;
@@ -380,7 +381,7 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     }
     if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->iters, 2 * B * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&ctx->order, B * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
+        hipMalloc(&ctx->order, (2 * (size_t)B + 1) * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
     (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
     (void)hipMemset(ctx->iters, 0, 2 * B * sizeof(int32_t));   // [0, B): last step, [B, 2B): running sum
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {

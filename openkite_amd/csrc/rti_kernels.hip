@@ -1162,25 +1162,28 @@ extern "C" int kite_debug_cd_profile(unsigned long long* out) {
 // (kiteNMPF.cpp:319-355) and status.
 // The normal matrix is factored in LDS (packed lower triangle).
 // ---------------------------------------------------------------------------
-// Expansion dx_{k+1} = A_k dx_k + B_k du_k + d_k (theta rows exact), trajectory
-// and control update, diagnostics (kiteNMPF.cpp:319-355) and status.  One
-// wavefront; w = scaled QP step in slots (i = l + 64 s); vec/col: LDS scratch.
-// WAVE: the caller is one wavefront of a larger block (the other waves have
-// left), so the LDS exchanges are ordered by a wavefront fence, not s_barrier.
+// Epilogue of every QP kernel, in two phases so that the state-bound check can
+// run on the expanded trajectory BEFORE anything is written (lazy rows):
+//   rti_expand : physical step dw = D w into vec[0, n); dx of the kite states
+//                (dx_0 = 0, dx_{k+1} = A_k dx_k + B_k du_k + d_k) and the exact
+//                theta / thetadot increments into dxs[k * 16 + (0..14)]
+//   rti_commit : trajectory and control update, diagnostics
+//                (kiteNMPF.cpp:319-355), status.
+// One wavefront; w = scaled QP step in slots (i = l + 64 s); vec, dxs: LDS
+// scratch (dxs: (N+1) x 16).  WAVE: the LDS exchanges are ordered by a
+// wavefront fence, not s_barrier (the caller is one wavefront of a larger
+// block).  Returns (wave-uniform) whether the expanded trajectory leaves the
+// bounds of states 1..12 anywhere (sbnd: fill_bounds) -- checked on the fly,
+// so the common case pays no separate pass (lazy_select runs only then).
+__device__ __forceinline__ double bound_tol(double b);
 template <int NS, bool WAVE = false>
-__device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, const double w[NS], double kkt, int iters,
-                             const double* __restrict__ AB, const double* __restrict__ DEF,
-                             double* __restrict__ Xb, double* __restrict__ Ub, double* __restrict__ u0_out,
-                             double* __restrict__ diag, int32_t* __restrict__ status,
-                             double* __restrict__ kkt_out, int32_t* __restrict__ iters_out,
-                             int32_t* __restrict__ iters_acc,
-                             double* vec, double* col) {
+__device__ __forceinline__ bool rti_expand(const RtiConst& C, int b, int l, const double w[NS], bool accept,
+                                           const double* __restrict__ AB, const double* __restrict__ DEF,
+                                           const double* __restrict__ Xb, const double* sbnd, double* vec,
+                                           double* dxs) {
     const int N = C.N, n = C.n;
-    // ---- expansion and trajectory update ------------------------------------
     // step safeguard (oracle rti_one): a failed QP (residual >= 1e-6 or NaN)
     // contributes no step; the shifted plan is kept and the gaps are closed
-    const bool accept = kkt < QP_STEP_ACCEPT;
-    // physical step dw = D w_s into vec
     if constexpr (WAVE) wave_sync(); else __syncthreads();
     {
         // column scale by value selects (a lane-dependent index into the
@@ -1206,40 +1209,37 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
             dth += C.dt * C.dt * ((double)(k - m) - 0.5) * du;
             dthd += C.dt * du;
         }
-        Xb[k * NX + 13] += dth;
-        Xb[k * NX + 14] += dthd;
+        dxs[k * 16 + 13] = dth;
+        dxs[k * 16 + 14] = dthd;
     }
-    // controls
-    for (int e = l; e < N * NU; e += 64) {
-        const int k = e / NU, c = e % NU;
-        Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
-    }
-    // kite states: dx_0 = 0, dx_{k+1} = A dx_k + B du_k + d_k (lane = row).
-    // The recursion is a chain of N dependent steps: dx_k is broadcast from
-    // lanes 0..12 by v_readlane (no LDS round trip, no barrier), the row dot
-    // product runs as four partial sums, and row l of [A_k | B_k], d_k and
-    // x_{k+1} come from a register ring PD intervals ahead (one interval of
-    // look-ahead would expose a global-memory latency per interval; the QP's
-    // registers are free by now).
+    // kite states: lane = row.  The recursion is a chain of N dependent steps:
+    // dx_k is broadcast from lanes 0..12 by v_readlane (no LDS round trip), the
+    // row dot product runs as four partial sums, and row l of [A_k | B_k] and
+    // d_k come from a register ring PD intervals ahead (one interval of
+    // look-ahead would expose a global-memory latency per interval).
+    bool viol = false;
     {
         constexpr int PD = 4;
         double dx = 0.0;
         const double* ABb = AB + (size_t)b * N * NK * 16;
         const double* DEFb = DEF + (size_t)b * N * NK;
         const int lr = l < NK ? l : NK - 1;
-        double ar[PD][16], dk[PD], xk1[PD];
-        auto fetch = [&](int k, double* a, double& d, double& x) __attribute__((always_inline)) {
+        const double blo = sbnd[lr], bhi = sbnd[16 + lr];
+        const double tlo = blo - bound_tol(blo), thi = bhi + bound_tol(bhi);
+        const bool chk = l >= 1 && l < NK;             // states 1..12 (vx: a QP row)
+        double ar[PD][16], dk[PD], xr[PD];
+        auto fetch = [&](int k, double* a, double& d, double& xn) __attribute__((always_inline)) {
             const double* p = ABb + ((size_t)k * NK + lr) * 16;
 #pragma unroll
             for (int j = 0; j < 16; ++j) a[j] = p[j];
             d = DEFb[(size_t)k * NK + lr];
-            x = Xb[(k + 1) * NX + lr];
+            xn = Xb[(k + 1) * NX + lr];
         };
         auto interval = [&](int k, double* ring, double& dring, double& xring) __attribute__((always_inline)) {
             double a[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) a[j] = ring[j];
-            const double d = dring, xo = xring;
+            const double d = dring, xn = xring;
             if (k + PD < N) fetch(k + PD, ring, dring, xring);
             double t0 = fma(a[NK], vec[3 * k], d), t1 = a[NK + 1] * vec[3 * k + 1];
             double t2 = a[NK + 2] * vec[3 * k + 2], t3 = 0.0;
@@ -1251,20 +1251,51 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
                 if (j + 3 < NK) t3 = fma(a[j + 3], readlane_d(dx, j + 3), t3);
             }
             dx = (t0 + t1) + (t2 + t3);
-            if (l < NK) Xb[(k + 1) * NX + l] = xo + dx;
+            if (l < NK) dxs[(k + 1) * 16 + l] = dx;
+            const double xt = xn + dx;
+            viol |= chk && (xt < tlo || xt > thi);
         };
+        if (l < NK) dxs[l] = 0.0;
 #pragma unroll
         for (int q = 0; q < PD; ++q)
-            if (q < N) fetch(q, ar[q], dk[q], xk1[q]);
+            if (q < N) fetch(q, ar[q], dk[q], xr[q]);
         for (int k0 = 0; k0 < N; k0 += PD) {
-            interval(k0, ar[0], dk[0], xk1[0]);
+            interval(k0, ar[0], dk[0], xr[0]);
             if (k0 + 1 >= N) break;
-            interval(k0 + 1, ar[1], dk[1], xk1[1]);
+            interval(k0 + 1, ar[1], dk[1], xr[1]);
             if (k0 + 2 >= N) break;
-            interval(k0 + 2, ar[2], dk[2], xk1[2]);
+            interval(k0 + 2, ar[2], dk[2], xr[2]);
             if (k0 + 3 >= N) break;
-            interval(k0 + 3, ar[3], dk[3], xk1[3]);
+            interval(k0 + 3, ar[3], dk[3], xr[3]);
         }
+    }
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
+    return wave_or(viol ? 1 : 0) != 0;
+}
+
+// state-bound tolerance (oracle bound_tol)
+__device__ __forceinline__ double bound_tol(double b) { return 1e-8 * fmax(1.0, fabs(b)); }
+
+template <bool WAVE = false>
+__device__ __forceinline__ void rti_commit(const RtiConst& C, int b, int l, double kkt, int iters,
+                                           const double* vec, const double* dxs, const double* sbnd,
+                                           double* __restrict__ Xb, double* __restrict__ Ub,
+                                           double* __restrict__ u0_out, double* __restrict__ diag,
+                                           int32_t* __restrict__ status, double* __restrict__ kkt_out,
+                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ iters_acc) {
+    const int N = C.N;
+    const bool accept = kkt < QP_STEP_ACCEPT;
+    for (int k = l; k <= N; k += 64) {
+        Xb[k * NX + 13] += dxs[k * 16 + 13];
+        Xb[k * NX + 14] += dxs[k * 16 + 14];
+    }
+    for (int e = l; e < N * NU; e += 64) {
+        const int k = e / NU, c = e % NU;
+        Ub[e] += (c < 3) ? vec[3 * k + c] : vec[3 * N + k];
+    }
+    for (int e = l; e < N * NK; e += 64) {
+        const int k = e / NK, i = e % NK;
+        Xb[(k + 1) * NX + i] += dxs[(k + 1) * 16 + i];
     }
     if constexpr (WAVE) wave_sync(); else __syncthreads();
 
@@ -1292,7 +1323,10 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         for (int i = 0; i < NX; ++i) if (!isfinite(xk[i])) bad = 1;
         if (k < N) for (int c = 0; c < NU; ++c) if (!isfinite(Ub[k * NU + c])) bad = 1;
         if (k >= 1)
-            for (int i = 1; i < 13; ++i) if (xk[i] < C.lbx[i] || xk[i] > C.ubx[i]) bound = 1;
+            for (int i = 1; i < 13; ++i) {
+                const double lb = sbnd[i], ub = sbnd[16 + i];
+                if (xk[i] < lb - bound_tol(lb) || xk[i] > ub + bound_tol(ub)) bound = 1;
+            }
     }
     cost = wave_sum(cost);
     bad = wave_or(bad);
@@ -1320,6 +1354,103 @@ __device__ __forceinline__ void rti_epilogue(const RtiConst& C, int b, int l, co
         if (iters_acc) iters_acc[b] += iters;          // running sum since kite_nmpc_timing_start
         for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
     }
+}
+
+// ---- lazy state-bound rows (oracle rti_one, LAZY_ROWS / LAZY_ROUNDS) --------
+// The vx bound is a QP row at every node; the other finite state bounds are
+// enforced on demand: after an accepted QP solve the expanded trajectory is
+// checked (states 1..12, nodes 1..N), the most violated (node, state) pairs
+// -- largest normalised violation first, ties by node then state, at most
+// LAZY_ROWS per RTI step -- become QP rows +-G_k[i,:] D w >= c, and the QP is
+// solved again from a cold start, at most LAZY_ROUNDS times.
+constexpr int LAZY_ROWS = 4, LAZY_ROUNDS = 2;
+constexpr int QP_LAZY_GRID = 256;                  // blocks of the lazy instances (grid-stride)
+// Every QP kernel comes in two instances.  LAZY = false (the whole grid)
+// solves, expands and checks the state bounds on the fly (rti_expand); a kite
+// with violations is appended to a list (lazy[0] = count, lazy[1..] = kites;
+// count reset by k_qp_order) and left uncommitted.  LAZY = true (launched
+// next, a 256-block grid-stride loop over the list) runs the full rule -- the
+// identical first solve, then the rounds with rows -- for the listed kites.
+// The fast instance thus has no re-solve loop (the back edge alone costs the
+// tiled kernel ~350 B/lane of spills) and the lazy one costs ~2 us when the
+// list is empty.
+// bound table (LDS): sbnd[i] = lbx[i], sbnd[16 + i] = ubx[i]
+__device__ __forceinline__ void fill_bounds(const RtiConst& C, int l, double* sbnd) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+        if (l == i) { sbnd[i] = C.lbx[i]; sbnd[16 + i] = C.ubx[i]; }
+}
+// Violations of the trajectory Xb + dxs -> viol[(k-1)*12 + (i-1)] (signed
+// normalised magnitude: > 0 below lb, < 0 above ub), then the `want` largest
+// into sel[3t + {0,1,2}] = {k, i, side}; returns their count (wave-uniform).
+template <bool WAVE = false>
+__device__ __attribute__((noinline)) int lazy_select(const RtiConst& C, int l, const double* Xb, const double* dxs, const double* sbnd,
+                           double* viol, int* sel, int want) {
+    const int N = C.N, np = N * 12;
+    for (int p = l; p < np; p += 64) {
+        const int k = 1 + p / 12, i = 1 + p % 12;
+        const double lb = sbnd[i], ub = sbnd[16 + i];
+        const double x = Xb[k * NX + i] + dxs[k * 16 + i];
+        double v = 0.0;
+        if (x < lb - bound_tol(lb)) v = (lb - x) / fmax(1.0, fabs(lb));
+        else if (x > ub + bound_tol(ub)) v = -(x - ub) / fmax(1.0, fabs(ub));
+        viol[p] = v;
+    }
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
+    int cnt = 0;
+    for (int t = 0; t < want; ++t) {
+        double best = 0.0, bp = 1e9;
+        for (int p = l; p < np; p += 64) {
+            const double a = fabs(viol[p]);
+            if (a > best) { best = a; bp = (double)p; }
+        }
+        const double M = wave_max(best);
+        if (!(M > 0.0)) break;
+        const int pm = (int)wave_min(best == M ? bp : 1e9);
+        if constexpr (WAVE) wave_sync(); else __syncthreads();
+        if (l == 0) {
+            sel[3 * t] = 1 + pm / 12;
+            sel[3 * t + 1] = 1 + pm % 12;
+            sel[3 * t + 2] = viol[pm] > 0.0 ? 1 : -1;
+            viol[pm] = 0.0;
+        }
+        if constexpr (WAVE) wave_sync(); else __syncthreads();
+        ++cnt;
+    }
+    return cnt;
+}
+// QP row of the violated (node k, state i, side): row[3j + c] = side G_k[i, (j, c)] / Su_c
+// for the kite controls (zero from column 3k on; theta and Uv columns are zero
+// for kite states), by the backward recursion lambda_j = A_j' lambda_{j+1},
+// lambda_k = e_i; returns the bound c of  row . w >= c  (wsc: scaled w, LDS).
+// row[0, ncol) is written (ncol >= 3N: the caller's row stride).
+template <bool WAVE = false>
+__device__ double lazy_row(const RtiConst& C, int b, int l, int k, int i, int side, const double* __restrict__ AB,
+                           const double* Xb, const double* dxs, const double* sbnd, const double* wsc,
+                           double* row, int ncol) {
+    const int N = C.N;
+    const double iS0 = 1.0 / C.Su[0], iS1 = 1.0 / C.Su[1], iS2 = 1.0 / C.Su[2];
+    for (int j = l; j < ncol; j += 64) row[j] = 0.0;
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
+    double lam = (l == i) ? (double)side : 0.0;
+    const double* ABb = AB + (size_t)b * N * NK * 16;
+    for (int j = k - 1; j >= 0; --j) {
+        const double* a = ABb + (size_t)j * NK * 16 + (l & 15);
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < NK; ++r) acc = fma(readlane_d(lam, r), a[r * 16], acc);
+        if (l >= NK && l < 16) {
+            const int c = l - NK;
+            row[3 * j + c] = acc * (c == 0 ? iS0 : (c == 1 ? iS1 : iS2));
+        }
+        lam = l < NK ? acc : 0.0;
+    }
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
+    const double bnd = side > 0 ? sbnd[i] : sbnd[16 + i];
+    const double xtry = Xb[k * NX + i] + dxs[k * 16 + i];
+    double dot = 0.0;
+    for (int j = l; j < 3 * k; j += 64) dot = fma(row[j], wsc[j], dot);
+    return (double)side * (bnd - xtry) + wave_sum(dot);
 }
 
 constexpr double IPM_S0 = 0.1, IPM_Z0 = 10.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
@@ -1367,8 +1498,8 @@ struct QPState {
 
 // NQ: largest n = 4N + 2 of the instantiation (82: N <= 20, 162: N <= 40);
 // C (vx-bound rows) is stored on its 3N kite columns only.
-template <int NQ>
-__global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
+template <int NQ, bool LAZY>
+__device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int B,
                                            const double* __restrict__ Hs, const double* __restrict__ hs,
                                            const double* __restrict__ Cr, const double* __restrict__ clp,
                                            const double* __restrict__ cup, const double* __restrict__ hmaxp,
@@ -1376,17 +1507,17 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                                            double* __restrict__ X, double* __restrict__ U,
                                            double* __restrict__ u0_out, double* __restrict__ diag,
                                            int32_t* __restrict__ status, double* __restrict__ kkt_out,
-                                           int32_t* __restrict__ iters_out,
-                                           const int32_t* __restrict__ order) {
+                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ lazy) {
     constexpr int NS = (NQ + 63) / 64;                 // variable slots per lane
     constexpr int NQN = (NQ - 2) / 4;                  // largest horizon
     __shared__ double Lp[NQ * (NQ + 1) / 2];
-    __shared__ double sC[NQN * 3 * NQN];
+    __shared__ double sC[(NQN + LAZY_ROWS) * 3 * NQN];   // vx rows, then the lazy state-bound rows
     __shared__ double vec[NQ + 2];
     __shared__ double col[NQ];
     __shared__ double dinv[NQ];
+    __shared__ double sbnd[32], sXc[LAZY_ROWS];
+    __shared__ int sel[3 * LAZY_ROWS];
 
-    const int b = order ? order[blockIdx.x] : blockIdx.x;     // longest-first dispatch (k_qp_order)
     const int l = threadIdx.x;
     const int N = C.N, n = C.n;
     const double* Hb = Hs + (size_t)b * n * n;
@@ -1396,11 +1527,15 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
 
     const int nc = 3 * N;                             // C columns kept (kite controls)
     for (int e = l; e < N * nc; e += 64) sC[e] = Crb[(e / nc) * n + e % nc];
+    fill_bounds(C, l, sbnd);
 
     QPState<NS> q;
     const bool has_lo = C.lo_fin != 0, has_hi = C.hi_fin != 0;
-    const int nI = 2 * n + N * ((has_lo ? 1 : 0) + (has_hi ? 1 : 0));
-    const bool row_lane = l < N;
+    int m = N;                                        // rows in use: N vx rows + lazy rows
+    int nI = 2 * n + N * ((has_lo ? 1 : 0) + (has_hi ? 1 : 0));
+    bool row_lane = l < N;
+    bool rlo = row_lane && has_lo, rhi = row_lane && has_hi;   // this row lane's finite sides
+    auto init_ipm = [&]() {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const int i = l + 64 * s;
@@ -1431,8 +1566,10 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         q.su[s] = fmax(hi - q.w[s], IPM_S0);
         q.zl[s] = IPM_Z0; q.zu[s] = IPM_Z0;
     }
-    q.clo = row_lane ? clp[(size_t)b * N + l] : 0.0;
-    q.chi = row_lane ? cup[(size_t)b * N + l] : 0.0;
+    q.clo = l < N ? clp[(size_t)b * N + l] : (row_lane ? sXc[l - N] : 0.0);
+    q.chi = l < N ? cup[(size_t)b * N + l] : 0.0;
+    };
+    init_ipm();
     const double dscale = 1.0 / (1.0 + hmaxp[b]);
 
     // --- helpers ---------------------------------------------------------
@@ -1453,7 +1590,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             double t = 0.0;
             if (i < n)
                 if (i < nc)
-                    for (int k = 0; k < N; ++k) t = fma(sC[k * nc + i], vec[k], t);
+                    for (int k = 0; k < m; ++k) t = fma(sC[k * nc + i], vec[k], t);
             out[s] = t;
         }
     };
@@ -1463,14 +1600,17 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     };
 
     // initial slacks of general rows
-    put_vec2(q.w);
-    __syncthreads();
-    q.cw = rows_times();
-    q.slo = row_lane && has_lo ? fmax(q.cw - q.clo, IPM_S0) : 1.0;
-    q.shi = row_lane && has_hi ? fmax(q.chi - q.cw, IPM_S0) : 1.0;
-    q.zlo = row_lane && has_lo ? IPM_Z0 : 0.0;
-    q.zhi = row_lane && has_hi ? IPM_Z0 : 0.0;
-    __syncthreads();
+    auto init_rows = [&]() {
+        put_vec2(q.w);
+        __syncthreads();
+        q.cw = rows_times();
+        q.slo = rlo ? fmax(q.cw - q.clo, IPM_S0) : 1.0;
+        q.shi = rhi ? fmax(q.chi - q.cw, IPM_S0) : 1.0;
+        q.zlo = rlo ? IPM_Z0 : 0.0;
+        q.zhi = rhi ? IPM_Z0 : 0.0;
+        __syncthreads();
+    };
+    init_rows();
 
     double resid = 0.0;
     auto residuals = [&]() -> double {
@@ -1489,7 +1629,7 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
         }
         q.cw = rows_times();
         __syncthreads();
-        if (row_lane) vec[l] = (has_lo ? q.zlo : 0.0) - (has_hi ? q.zhi : 0.0);
+        if (row_lane) vec[l] = (rlo ? q.zlo : 0.0) - (rhi ? q.zhi : 0.0);
         __syncthreads();
         double ctz[NS];
         rows_T(ctz);
@@ -1510,10 +1650,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             }
         }
         q.rplo = 0.0; q.rphi = 0.0;
-        if (row_lane) {
-            if (has_lo) { q.rplo = q.cw - q.clo - q.slo; rmax = nmax(rmax, fabs(q.rplo)); mu += q.slo * q.zlo; }
-            if (has_hi) { q.rphi = q.chi - q.cw - q.shi; rmax = nmax(rmax, fabs(q.rphi)); mu += q.shi * q.zhi; }
-        }
+        if (rlo) { q.rplo = q.cw - q.clo - q.slo; rmax = nmax(rmax, fabs(q.rplo)); mu += q.slo * q.zlo; }
+        if (rhi) { q.rphi = q.chi - q.cw - q.shi; rmax = nmax(rmax, fabs(q.rphi)); mu += q.shi * q.zhi; }
         rmax = wave_nmax(rmax);
         mu = wave_sum(mu) / (double)nI;
         resid = nmax(rmax, mu);
@@ -1578,10 +1716,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
     struct Dir { double dw[NS], dsl[NS], dsu[NS], dzl[NS], dzu[NS], dslo, dshi, dzlo, dzhi; };
     auto newton = [&](const double rcl[NS], const double rcu[NS], double rclo, double rchi, Dir& D) {
         double t_lo = 0.0, t_hi = 0.0;
-        if (row_lane) {
-            if (has_lo) t_lo = rclo / q.slo - sglo * q.rplo;
-            if (has_hi) t_hi = rchi / q.shi - sghi * q.rphi;
-        }
+        if (rlo) t_lo = rclo / q.slo - sglo * q.rplo;
+        if (rhi) t_hi = rchi / q.shi - sghi * q.rphi;
         __syncthreads();
         if (row_lane) vec[l] = t_lo - t_hi;
         __syncthreads();
@@ -1613,10 +1749,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             D.dzu[s] = (rcu[s] - q.zu[s] * D.dsu[s]) / q.su[s];
         }
         D.dslo = 0.0; D.dshi = 0.0; D.dzlo = 0.0; D.dzhi = 0.0;
-        if (row_lane) {
-            if (has_lo) { D.dslo = cdw + q.rplo; D.dzlo = (rclo - q.zlo * D.dslo) / q.slo; }
-            if (has_hi) { D.dshi = -cdw + q.rphi; D.dzhi = (rchi - q.zhi * D.dshi) / q.shi; }
-        }
+        if (rlo) { D.dslo = cdw + q.rplo; D.dzlo = (rclo - q.zlo * D.dslo) / q.slo; }
+        if (rhi) { D.dshi = -cdw + q.rphi; D.dzhi = (rchi - q.zhi * D.dshi) / q.shi; }
     };
     auto max_step = [&](const Dir& D) -> double {
         double a = 1.0;
@@ -1630,20 +1764,23 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                 if (D.dzu[s] < 0.0) a = fmin(a, -q.zu[s] / D.dzu[s]);
             }
         }
-        if (row_lane) {
-            if (has_lo) {
-                if (D.dslo < 0.0) a = fmin(a, -q.slo / D.dslo);
-                if (D.dzlo < 0.0) a = fmin(a, -q.zlo / D.dzlo);
-            }
-            if (has_hi) {
-                if (D.dshi < 0.0) a = fmin(a, -q.shi / D.dshi);
-                if (D.dzhi < 0.0) a = fmin(a, -q.zhi / D.dzhi);
-            }
+        if (rlo) {
+            if (D.dslo < 0.0) a = fmin(a, -q.slo / D.dslo);
+            if (D.dzlo < 0.0) a = fmin(a, -q.zlo / D.dzlo);
+        }
+        if (rhi) {
+            if (D.dshi < 0.0) a = fmin(a, -q.shi / D.dshi);
+            if (D.dzhi < 0.0) a = fmin(a, -q.zhi / D.dzhi);
         }
         return wave_min(a);
     };
 
     int iters = C.K;
+    double kkt = 0.0;
+    double* dxs = Lp;                                 // the factor is dead after the last solve
+    double* viol = Lp + (N + 1) * 16;
+    for (int round = 0, added = 0;; ++round) {
+    iters = C.K;
     for (int it = 0; it < C.K; ++it) {
         const double mu = residuals();
         if (resid < IPM_FREEZE || resid != resid) { iters = it; break; }   // converged, or poisoned
@@ -1653,8 +1790,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             sgl[s] = q.zl[s] / q.sl[s];
             sgu[s] = q.zu[s] / q.su[s];
         }
-        sglo = (row_lane && has_lo) ? q.zlo / q.slo : 0.0;
-        sghi = (row_lane && has_hi) ? q.zhi / q.shi : 0.0;
+        sglo = rlo ? q.zlo / q.slo : 0.0;
+        sghi = rhi ? q.zhi / q.shi : 0.0;
         __syncthreads();
         if (row_lane) vec[l] = sglo + sghi;
         __syncthreads();
@@ -1664,11 +1801,11 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             for (int s = 0; s < NS; ++s) {
                 const int c = l + 64 * s;
                 if (c <= rr) {
-                    double m = hr[c];
+                    double mv = hr[c];
                     if (rr < nc && c < nc)
-                        for (int k = 0; k < N; ++k) m = fma(sC[k * nc + rr] * vec[k], sC[k * nc + c], m);
-                    if (c == rr) m += sgl[s] + sgu[s];
-                    Lp[pk(rr, c)] = m;
+                        for (int k = 0; k < m; ++k) mv = fma(sC[k * nc + rr] * vec[k], sC[k * nc + c], mv);
+                    if (c == rr) mv += sgl[s] + sgu[s];
+                    Lp[pk(rr, c)] = mv;
                 }
             }
         }
@@ -1690,10 +1827,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
                 mua += (q.sl[s] + aa * Da.dsl[s]) * (q.zl[s] + aa * Da.dzl[s]) +
                        (q.su[s] + aa * Da.dsu[s]) * (q.zu[s] + aa * Da.dzu[s]);
         }
-        if (row_lane) {
-            if (has_lo) mua += (q.slo + aa * Da.dslo) * (q.zlo + aa * Da.dzlo);
-            if (has_hi) mua += (q.shi + aa * Da.dshi) * (q.zhi + aa * Da.dzhi);
-        }
+        if (rlo) mua += (q.slo + aa * Da.dslo) * (q.zlo + aa * Da.dzlo);
+        if (rhi) mua += (q.shi + aa * Da.dshi) * (q.zhi + aa * Da.dzhi);
         mua = wave_sum(mua) / (double)nI;
         double sigma = mua / mu;
         sigma = sigma * sigma * sigma;
@@ -1703,8 +1838,8 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             rcl[s] = -q.sl[s] * q.zl[s] - Da.dsl[s] * Da.dzl[s] + sigma * mu;
             rcu[s] = -q.su[s] * q.zu[s] - Da.dsu[s] * Da.dzu[s] + sigma * mu;
         }
-        rclo = row_lane && has_lo ? -q.slo * q.zlo - Da.dslo * Da.dzlo + sigma * mu : 0.0;
-        rchi = row_lane && has_hi ? -q.shi * q.zhi - Da.dshi * Da.dzhi + sigma * mu : 0.0;
+        rclo = rlo ? -q.slo * q.zlo - Da.dslo * Da.dzlo + sigma * mu : 0.0;
+        rchi = rhi ? -q.shi * q.zhi - Da.dshi * Da.dzhi + sigma * mu : 0.0;
         Dir Dc;
         newton(rcl, rcu, rclo, rchi, Dc);
         const double a = fmin(1.0, fmax(IPM_TAU, 1.0 - mu) * max_step(Dc));   // tau_k -> 1 (oracle qp_ipm)
@@ -1714,17 +1849,63 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst /*P*/, RtiConst C, int B,
             q.sl[s] += a * Dc.dsl[s]; q.su[s] += a * Dc.dsu[s];
             q.zl[s] += a * Dc.dzl[s]; q.zu[s] += a * Dc.dzu[s];
         }
-        if (row_lane) {
-            if (has_lo) { q.slo += a * Dc.dslo; q.zlo += a * Dc.dzlo; }
-            if (has_hi) { q.shi += a * Dc.dshi; q.zhi += a * Dc.dzhi; }
-        }
+        if (rlo) { q.slo += a * Dc.dslo; q.zlo += a * Dc.dzlo; }
+        if (rhi) { q.shi += a * Dc.dshi; q.zhi += a * Dc.dzhi; }
     }
     // final residual (also when frozen: residuals() already ran)
     residuals();
-    const double kkt = resid;
+    kkt = resid;
+    __syncthreads();
+    const bool outside = rti_expand<NS>(C, b, l, q.w, kkt < QP_STEP_ACCEPT, AB, DEF, Xb, sbnd, vec, dxs);
+    if (!outside || !(kkt < QP_STEP_ACCEPT) || round == LAZY_ROUNDS || added == LAZY_ROWS) break;
+    const int cnt = lazy_select(C, l, Xb, dxs, sbnd, viol, sel, LAZY_ROWS - added);
+    if (cnt == 0) break;
+    if constexpr (!LAZY) { if (l == 0) lazy[1 + atomicAdd(lazy, 1)] = b; return; }   // to the lazy instance
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { const int i = l + 64 * s; if (i < n) col[i] = q.w[s]; }   // scaled w
+    __syncthreads();
+    for (int t = 0; t < cnt; ++t) {
+        const double cv = lazy_row(C, b, l, sel[3 * t], sel[3 * t + 1], sel[3 * t + 2], AB, Xb, dxs, sbnd, col,
+                                   sC + (size_t)m * nc, nc);
+        if (l == 0) sXc[m - N] = cv;
+        ++m;
+        __syncthreads();
+    }
+    added += cnt;
+    // the QP again with the new rows (cold start)
+    nI += cnt;
+    row_lane = l < m;
+    rlo = l < N ? (row_lane && has_lo) : row_lane;
+    rhi = l < N ? (row_lane && has_hi) : false;
+    init_ipm();
+    init_rows();
+    }
+    rti_commit(C, b, l, kkt, iters, vec, dxs, sbnd, Xb, Ub, u0_out, diag, status, kkt_out, iters_out,
+               iters_out ? iters_out + B : nullptr);
+}
 
-    rti_epilogue<NS>(C, b, l, q.w, kkt, iters, AB, DEF, Xb, Ub, u0_out, diag, status, kkt_out, iters_out,
-                     iters_out ? iters_out + B : nullptr, vec, col);
+// the fast instance over the whole grid (LPT order); the lazy instance over
+// the kites the fast one listed (lazy[0] = count, lazy[1..]), grid-strided
+template <int NQ, bool LAZY>
+__global__ __launch_bounds__(64) void k_qp(ModelConst P, RtiConst C, int B,
+                                           const double* __restrict__ Hs, const double* __restrict__ hs,
+                                           const double* __restrict__ Cr, const double* __restrict__ clp,
+                                           const double* __restrict__ cup, const double* __restrict__ hmaxp,
+                                           const double* __restrict__ AB, const double* __restrict__ DEF,
+                                           double* __restrict__ X, double* __restrict__ U,
+                                           double* __restrict__ u0_out, double* __restrict__ diag,
+                                           int32_t* __restrict__ status, double* __restrict__ kkt_out,
+                                           int32_t* __restrict__ iters_out,
+                                           const int32_t* __restrict__ order, int32_t* __restrict__ lazy) {
+    if constexpr (LAZY) {
+        const int cnt = lazy[0];
+        for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+            qp_body<NQ, true>(lazy[1 + j], P, C, B, Hs, hs, Cr, clp, cup, hmaxp, AB, DEF, X, U, u0_out, diag, status, kkt_out, iters_out, lazy);
+            __syncthreads();
+        }
+    } else {
+        qp_body<NQ, false>(order ? order[blockIdx.x] : blockIdx.x, P, C, B, Hs, hs, Cr, clp, cup, hmaxp, AB, DEF, X, U, u0_out, diag, status, kkt_out, iters_out, lazy);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1875,15 +2056,22 @@ hipError_t launch_condense(const RtiConst& C, int B, const double* X, const doub
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
-                     int32_t* status, double* kkt, int32_t* iters, const int32_t* order, hipStream_t s) {
-    if (C.n <= 82)
-        hipLaunchKernelGGL(k_qp<82>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U, u0,
-                           diag, status, kkt, iters, order);
-    else if (C.n <= 162)
-        hipLaunchKernelGGL(k_qp<162>, dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X, U,
-                           u0, diag, status, kkt, iters, order);
-    else
+                     int32_t* status, double* kkt, int32_t* iters, const int32_t* order, int32_t* lazy,
+                     hipStream_t s) {
+    const int G = B < QP_LAZY_GRID ? B : QP_LAZY_GRID;
+    if (C.n <= 82) {
+        hipLaunchKernelGGL((k_qp<82, false>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
+                           U, u0, diag, status, kkt, iters, order, lazy);
+        hipLaunchKernelGGL((k_qp<82, true>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
+                           U, u0, diag, status, kkt, iters, order, lazy);
+    } else if (C.n <= 162) {
+        hipLaunchKernelGGL((k_qp<162, false>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
+                           X, U, u0, diag, status, kkt, iters, order, lazy);
+        hipLaunchKernelGGL((k_qp<162, true>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
+                           X, U, u0, diag, status, kkt, iters, order, lazy);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 // Dispatch order of the QP grid: kites by their previous step's IPM iteration
@@ -1893,9 +2081,10 @@ hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double
 // ones first (largest-processing-time-first list scheduling) keeps the short
 // ones for the tail, where otherwise SIMDs idle while a late long kite ends.
 __global__ __launch_bounds__(1024) void k_qp_order(int B, int K, const int32_t* __restrict__ iters,
-                                                   int32_t* __restrict__ order) {
+                                                   int32_t* __restrict__ order, int32_t* __restrict__ lazy) {
     __shared__ int cnt[257];
     const int t = threadIdx.x;
+    if (t == 0) lazy[0] = 0;
     const int nb = (K < 255 ? K : 255) + 1;
     for (int i = t; i <= nb; i += 1024) cnt[i] = 0;
     __syncthreads();
@@ -1909,8 +2098,9 @@ __global__ __launch_bounds__(1024) void k_qp_order(int B, int K, const int32_t* 
     __syncthreads();
     for (int b = t; b < B; b += 1024) order[atomicAdd(&cnt[key(b)], 1)] = b;
 }
-hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, hipStream_t s) {
-    hipLaunchKernelGGL(k_qp_order, dim3(1), dim3(1024), 0, s, B, C.K, iters, order);
+hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, int32_t* lazy,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_qp_order, dim3(1), dim3(1024), 0, s, B, C.K, iters, order, lazy);
     return hipGetLastError();
 }
 hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,

@@ -48,13 +48,16 @@ hipError_t launch_qp_tiled(const ModelConst& P, const RtiConst& C, int B, const 
                            const double* Hbb, const double* hs, const double* Cr, const double* cl,
                            const double* cu, const double* hmax, const double* AB, const double* DEF, double* X,
                            double* U, double* u0, double* diag, int32_t* status, double* kkt, int32_t* iters,
-                           const int32_t* order, hipStream_t s);
+                           const int32_t* order, int32_t* lazy, hipStream_t s);
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
-                     int32_t* status, double* kkt, int32_t* iters, const int32_t* order, hipStream_t s);
-// QP grid dispatch order: kites by the previous step's iteration count, most first
-hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, hipStream_t s);
+                     int32_t* status, double* kkt, int32_t* iters, const int32_t* order, int32_t* lazy,
+                     hipStream_t s);
+// QP grid dispatch order: kites by the previous step's iteration count, most
+// first; also empties the lazy state-bound list (lazy[0] = 0, B + 1 entries)
+hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, int32_t* lazy,
+                           hipStream_t s);
 hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,
                            hipStream_t s);
 hipError_t launch_jacobian(const ModelConst& P, int count, const double* x, const double* u, double* Jx,

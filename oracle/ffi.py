@@ -106,7 +106,7 @@ def lib():
             "orc_rk4_sens_cs": (None, [dp, dp, dp, d, i, dp, dp]),
             "orc_path": (None, [dp, d, dp, dp]),
             "orc_closest_point": (d, [dp, dp, d]),
-            "orc_build_qp": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
+            "orc_build_qp": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
             "orc_qp_solve": (d, [i, i, dp, dp, dp, dp, dp, dp, i, dp]),
             "orc_prologue": (i, [dp, dp, i, i, dp, i, i, dp, dp, dp]),
             "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i]),
@@ -215,14 +215,17 @@ def closest_point(cfgv, pos, guess=0.0):
     return lib().orc_closest_point(_p(cfgv), _p(_f64(pos)), float(guess))
 
 
-def build_qp(kp, cfgv, N, M, X, U):
+def build_qp(kp, cfgv, N, M, X, U, want_G=False):
+    """Condensed QP of the oracle (scaled variables, oracle column order);
+    want_G: also G = d x / d dw, shape (N + 1, 15, n) (unscaled dw = D w)."""
     n = 4 * N + 2
     mmax = 2 * N
     H = np.zeros((n, n)); h = np.zeros(n); lb = np.zeros(n); ub = np.zeros(n)
     C = np.zeros((mmax, n)); c = np.zeros(mmax); D = np.zeros(n); g = np.zeros((N + 1, 15))
+    G = np.zeros((N + 1, 15, n)) if want_G else None
     m = lib().orc_build_qp(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), _p(H), _p(h), _p(lb),
-                           _p(ub), _p(C), _p(c), _p(D), _p(g))
-    return dict(H=H, h=h, lb=lb, ub=ub, C=C[:m].copy(), c=c[:m].copy(), D=D, g=g, m=m)
+                           _p(ub), _p(C), _p(c), _p(D), _p(g), _p(G) if want_G else None)
+    return dict(H=H, h=h, lb=lb, ub=ub, C=C[:m].copy(), c=c[:m].copy(), D=D, g=g, m=m, G=G)
 
 
 def qp_solve(H, h, lb, ub, C, c, K):

@@ -255,6 +255,7 @@ def test_long_closed_loop_vs_oracle(kp, cfgv):
             r = g.step(x)
             u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0), nthreads=8)
             assert not np.any(r["status"] & 1) and not np.any(st & 1)
+            assert not np.any(r["status"] & 8) and not np.any(st & 8)    # state bounds never bind here
             same = (r["status"] & 32) == (st & 32)
             diverged |= ~same
             rejected += int(np.sum(st & 32))
@@ -508,6 +509,7 @@ def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_fra
             r = g.step(x)
             u0, diag, st = ffi.rti_step(kp, cfgv, N, M, K, x, Xo, Uo, warm=int(step > 0), nthreads=0)
             assert not np.any(r["status"] & 1) and not np.any(st & 1)
+            assert not np.any(r["status"] & 8) and not np.any(st & 8)    # state bounds never bind here
             same = (r["status"] & 32) == (st & 32)
             diverged |= ~same
             d = np.abs(r["traj"] - Xo).reshape(B, -1).max(1) / np.maximum(1.0, np.abs(Xo).reshape(B, -1).max(1))

@@ -50,12 +50,18 @@ def gpu_perm(N):
     return np.array(p)
 
 
-def kkt_certificate(H, h, lb, ub, C, c, w):
+def kkt_certificate(H, h, lb, ub, C, c, w, extra=None):
+    """extra: (A, s, bnd) further constraints A w >= ... with slacks s (the state
+    bounds the lazy rows enforce; bnd: the bound each slack refers to)."""
     from scipy.optimize import nnls
     n = w.size
     g = H @ w + h
     sl, su, sc = w - lb, ub - w, C @ w - c
     rows = []
+    if extra is not None:
+        for a, s_, bd in zip(*extra):
+            if s_ <= ACT_TOL * max(1.0, abs(bd)):
+                rows.append(a)
     for i in range(n):
         if sl[i] <= ACT_TOL * max(1.0, abs(lb[i])):
             e = np.zeros(n); e[i] = 1.0; rows.append(e)
@@ -89,6 +95,23 @@ def scaled_solution(cfg, N, U_lin, X_lin, U_new, X_new):
     lb[4 * N + 1], ub[4 * N + 1] = -cfg.theta_flex * cfg.Sx[14], cfg.theta_flex * cfg.Sx[14]
     p = gpu_perm(N)
     return w_or[p], lb[p], ub[p]
+
+
+def state_bound_rows(q_or, cfg, N, X_new):
+    """Finite bounds of states 1..12 at nodes 1..N as constraints on the scaled
+    GPU variables: +-G_k[i] D w >= ..., slacks from the trajectory the GPU
+    applied (the expansion is linear in w, so X_new = x(w) exactly)."""
+    p = gpu_perm(N)
+    A, s, bnd = [], [], []
+    for k in range(1, N + 1):
+        for i in range(1, 13):
+            row = (q_or["G"][k, i] * q_or["D"])[p]
+            lo, hi = cfg.lbx[i], cfg.ubx[i]
+            if np.isfinite(lo):
+                A.append(row); s.append(X_new[k, i] - lo); bnd.append(lo)
+            if np.isfinite(hi):
+                A.append(-row); s.append(hi - X_new[k, i]); bnd.append(hi)
+    return np.array(A), np.array(s), np.array(bnd)
 
 
 def test_certificate_on_oracle_closed_loop(kp):
@@ -146,7 +169,13 @@ def test_gpu_qp_solution_satisfies_kkt(kp, N, qp_kernel):
                 _, Xl, Ul, _ = ffi.prologue(kp, cv, N, M, x[b], Xprev[b], Uprev[b], warm=int(step > 0))
                 q = g.get_qp(b)
                 w, lb, ub = scaled_solution(cfg, N, Ul, Xl, r["ctrl"][b], r["traj"][b])
-                stat, feas, nact = kkt_certificate(q["H"], q["h"], lb, ub, q["C"], q["cl"], w)
+                # state bounds (lazy rows; at N = 40 the |q_i| <= 1.01 bound binds on the
+                # cold step): their multipliers enter stationarity, their slacks must be >= 0
+                A, sx, bnd = state_bound_rows(ffi.build_qp(kp, cv, N, M, Xl, Ul, want_G=True), cfg, N,
+                                              r["traj"][b])
+                if not r["status"][b] & 8:
+                    assert sx.min() >= -1e-8 * np.abs(bnd).max(), (step, b, sx.min())
+                stat, feas, nact = kkt_certificate(q["H"], q["h"], lb, ub, q["C"], q["cl"], w, (A, sx, bnd))
                 worst_stat, worst_feas = max(worst_stat, stat), max(worst_feas, feas)
                 bar = KKT_TOL_CAPPED if r["status"][b] & 2 else KKT_TOL
                 capped += int(r["status"][b] & 2 != 0)

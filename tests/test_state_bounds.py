@@ -1,0 +1,103 @@
+"""Finite state bounds other than vx: lazy QP rows (oracle/kite_oracle.cpp
+rti_one, LAZY_ROWS = 4 per step, LAZY_ROUNDS = 2 re-solves; the GPU QP kernels
+implement the same rule).
+
+The reference's bounds |omega_i| <= 4 pi and |q_i| <= 1.01 (nmpf_node.cpp:59-63)
+never bind on the benchmark workload (bit 8 stays clear, asserted by the
+full-batch GPU tests); a tight roll/pitch/yaw-rate bound |omega_i| <= 3 rad/s
+does, so it is the test case here: on identical inputs the default-bound plan
+leaves the tight box in a few dozen kite-steps, the lazy rows pull those back
+inside, and only kites where four rows per step do not suffice keep bit 8.
+"""
+import numpy as np
+import pytest
+
+import openkite_amd as ok
+from oracle import ffi
+
+M, K = 2, 16
+W_BOUND = 3.0
+RTI_TOL = 1e-6          # as tests/test_gpu_parity.py
+
+
+def tight_config(N):
+    c = ffi.node_config(N=N)
+    c["lbx"][3:6] = [-W_BOUND] * 3
+    c["ubx"][3:6] = [W_BOUND] * 3
+    return c
+
+
+def x0_batch(B, cv, offset):
+    xs = ffi.synthetic_states(B, offset=offset)
+    x0 = np.zeros((B, 15))
+    x0[:, :13] = xs
+    for b in range(B):
+        x0[b, 13] = ffi.closest_point(cv, xs[b, 6:9])
+    return x0
+
+
+def within_bound(X):
+    return np.abs(X[:, 1:, 3:6]).max(axis=(1, 2)) <= W_BOUND * (1 + 1e-8)
+
+
+def test_oracle_lazy_rows_enforce_tight_rate_bound(kp):
+    N, B = 20, 64
+    cv = ffi.cfg_vector(tight_config(N))
+    cd = ffi.cfg_vector(ffi.node_config(N=N))
+    x = x0_batch(B, cv, 11000)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    active = kept = 0
+    for step in range(8):
+        Xd, Ud = Xo.copy(), Uo.copy()
+        _, _, sd = ffi.rti_step(kp, cd, N, M, K, x, Xd, Ud, warm=int(step > 0))
+        assert not np.any(sd & 8)                      # reference bounds: never active
+        active += int((~within_bound(Xd)).sum())
+        _, _, st = ffi.rti_step(kp, cv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+        b8 = (st & 8) != 0
+        kept += int(b8.sum())
+        assert np.all(within_bound(Xo)[~b8])           # bit 8 <=> outside the box
+        assert not np.any(within_bound(Xo)[b8])
+        x = Xo[:, 1, :].copy()
+    assert active >= 10, active                        # the bound binds
+    assert kept <= active // 4, (kept, active)         # and the rows enforce it
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,qp_kernel", [(20, 1), (20, 2), (40, 1), (40, 2)])
+def test_gpu_lazy_rows_vs_oracle(kp, N, qp_kernel):
+    """Every QP kernel (1 = wave-scalar k_qp, 2 = k_qp_tiled at N = 20 /
+    k_qp_lds at N = 40) against the oracle with the tight rate bound, from
+    identical inputs every step (set_solution).  Status bits must agree
+    (bit 2 aside: the 1e-8 convergence flag near its threshold); trajectories
+    within RTI_TOL where both QPs froze, within 1e-2 for capped N = 40 QPs
+    (test_gpu_parity.py::test_n40_qp_kernels_vs_oracle)."""
+    B, steps = 64, (8 if N == 20 else 6)
+    c = tight_config(N)
+    cv = ffi.cfg_vector(c)
+    cfg = ok.default_config(N=N)
+    cfg.qp_kernel = qp_kernel
+    for i in range(3, 6):
+        cfg.lbx[i] = -W_BOUND
+        cfg.ubx[i] = W_BOUND
+    x = x0_batch(B, cv, 11000 if N == 20 else 12000)
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    bound_steps = 0
+    try:
+        for step in range(steps):
+            if step > 0:
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            _, diag, st = ffi.rti_step(kp, cv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            bound_steps += int(((st & 8) != 0).sum())
+            e = np.array([max(abs(r["traj"][k] - Xo[k]).max() / max(1.0, abs(Xo[k]).max()),
+                              abs(r["ctrl"][k] - Uo[k]).max() / max(1.0, abs(Uo[k]).max())) for k in range(B)])
+            conv = (r["diag"][:, 5] < 1e-10) & (diag[:, 5] < 1e-10)
+            assert e[conv].max(initial=0.0) < RTI_TOL and e.max() < 1e-2, (step, np.sort(e)[-4:])
+            ok_ = (r["status"] & 8) == 0
+            assert np.all(within_bound(r["traj"])[ok_])
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+    print(f"N={N} kernel {qp_kernel}: {bound_steps} kite-steps keep bit 8 of {B * steps}")
