@@ -1886,7 +1886,8 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
 
 // the fast instance over the whole grid (LPT order); the lazy instance over
 // the kites the fast one listed (lazy[0] = count, lazy[1..]), grid-strided
-template <int NQ, bool LAZY>
+// (separate names: profilers that truncate template arguments keep them apart)
+template <int NQ>
 __global__ __launch_bounds__(64) void k_qp(ModelConst P, RtiConst C, int B,
                                            const double* __restrict__ Hs, const double* __restrict__ hs,
                                            const double* __restrict__ Cr, const double* __restrict__ clp,
@@ -1897,15 +1898,24 @@ __global__ __launch_bounds__(64) void k_qp(ModelConst P, RtiConst C, int B,
                                            int32_t* __restrict__ status, double* __restrict__ kkt_out,
                                            int32_t* __restrict__ iters_out,
                                            const int32_t* __restrict__ order, int32_t* __restrict__ lazy) {
-    if constexpr (LAZY) {
+        qp_body<NQ, false>(order ? order[blockIdx.x] : blockIdx.x, P, C, B, Hs, hs, Cr, clp, cup, hmaxp, AB, DEF, X, U, u0_out, diag, status, kkt_out, iters_out, lazy);
+}
+template <int NQ>
+__global__ __launch_bounds__(64) void k_qp_lazy(ModelConst P, RtiConst C, int B,
+                                           const double* __restrict__ Hs, const double* __restrict__ hs,
+                                           const double* __restrict__ Cr, const double* __restrict__ clp,
+                                           const double* __restrict__ cup, const double* __restrict__ hmaxp,
+                                           const double* __restrict__ AB, const double* __restrict__ DEF,
+                                           double* __restrict__ X, double* __restrict__ U,
+                                           double* __restrict__ u0_out, double* __restrict__ diag,
+                                           int32_t* __restrict__ status, double* __restrict__ kkt_out,
+                                           int32_t* __restrict__ iters_out,
+                                           const int32_t* __restrict__ order, int32_t* __restrict__ lazy) {
         const int cnt = lazy[0];
         for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
             qp_body<NQ, true>(lazy[1 + j], P, C, B, Hs, hs, Cr, clp, cup, hmaxp, AB, DEF, X, U, u0_out, diag, status, kkt_out, iters_out, lazy);
             __syncthreads();
         }
-    } else {
-        qp_body<NQ, false>(order ? order[blockIdx.x] : blockIdx.x, P, C, B, Hs, hs, Cr, clp, cup, hmaxp, AB, DEF, X, U, u0_out, diag, status, kkt_out, iters_out, lazy);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2060,14 +2070,14 @@ hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double
                      hipStream_t s) {
     const int G = B < QP_LAZY_GRID ? B : QP_LAZY_GRID;
     if (C.n <= 82) {
-        hipLaunchKernelGGL((k_qp<82, false>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
+        hipLaunchKernelGGL((k_qp<82>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
                            U, u0, diag, status, kkt, iters, order, lazy);
-        hipLaunchKernelGGL((k_qp<82, true>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
+        hipLaunchKernelGGL((k_qp_lazy<82>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
                            U, u0, diag, status, kkt, iters, order, lazy);
     } else if (C.n <= 162) {
-        hipLaunchKernelGGL((k_qp<162, false>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
+        hipLaunchKernelGGL((k_qp<162>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
                            X, U, u0, diag, status, kkt, iters, order, lazy);
-        hipLaunchKernelGGL((k_qp<162, true>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
+        hipLaunchKernelGGL((k_qp_lazy<162>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
                            X, U, u0, diag, status, kkt, iters, order, lazy);
     } else {
         return hipErrorInvalidValue;
