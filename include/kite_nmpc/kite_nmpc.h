@@ -51,8 +51,10 @@ extern "C" {
 #define KITE_ST_NAN            1   /* non-finite value in the new iterate     */
 #define KITE_ST_QP_NOT_CONV    2   /* QP residual > 1e-8 after the cap K       */
 #define KITE_ST_MIN_SPEED      4   /* vx clamped to min_speed (nmpf_node.cpp:241-243) */
-#define KITE_ST_STATE_BOUND    8   /* predicted state outside lbx/ubx (states not
-                                      enforced in the QP: everything but vx) */
+#define KITE_ST_STATE_BOUND    8   /* new trajectory still outside lbx/ubx after the
+                                      lazy state-bound rows (vx: a QP row at every
+                                      node; states 1..12: at most 4 rows per step,
+                                      2 re-solves -- DESIGN.md 4.4)                */
 #define KITE_ST_THETA_WRAP    16   /* theta wrapped by 2*pi (kiteNMPF.cpp:212-221) */
 #define KITE_ST_STEP_REJECTED 32   /* QP residual >= 1e-6 or NaN: no step applied, the
                                       shifted plan is kept (the reference applies the
@@ -98,7 +100,8 @@ typedef struct kite_nmpc_config {
     double R[4];          /* control weights (kiteNMPF.cpp:33)                 */
     double W;             /* path-speed weight (kiteNMPF.cpp:34)               */
     double Sx[15], Su[4]; /* scaling diagonals (nmpf_node.cpp:50-51)           */
-    double lbx[15], ubx[15];  /* state bounds (nmpf_node.cpp:59-63); +-INFINITY = none */
+    double lbx[15], ubx[15];  /* state bounds (nmpf_node.cpp:59-63); +-INFINITY = none;
+                                 13, 14 (theta, thetadot) are not bounded    */
     double lbu[4], ubu[4];    /* control bounds (nmpf_node.cpp:45-47)          */
     double vref;          /* physical path speed (setReferenceVelocity, nmpf_node.cpp:68) */
     double path_radius;   /* P(theta) = rot(q)[R cos, R sin, alt] (nmpf_node.cpp:30-40) */

@@ -137,6 +137,12 @@ int validate_config(const kite_nmpc_config& c) {
         if (!(c.Su[i] != 0.0) || !std::isfinite(c.Su[i])) return KITE_EINVAL;
         if (!std::isfinite(c.lbu[i]) || !std::isfinite(c.ubu[i]) || !(c.lbu[i] < c.ubu[i])) return KITE_EINVAL;
     }
+    // state bounds: ordered, no NaN; theta / thetadot (13, 14) are free in the
+    // reference (nmpf_node.cpp:59-63) and not enforced here -- refuse finite ones
+    // rather than drop them silently
+    for (int i = 0; i < 15; ++i) if (!(c.lbx[i] <= c.ubx[i])) return KITE_EINVAL;
+    for (int i = 13; i < 15; ++i)
+        if (!(std::isinf(c.lbx[i]) && c.lbx[i] < 0.0 && std::isinf(c.ubx[i]) && c.ubx[i] > 0.0)) return KITE_EINVAL;
     for (int i = 0; i < 3; ++i) if (!(c.Q[i] >= 0.0)) return KITE_EINVAL;
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;

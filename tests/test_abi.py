@@ -112,6 +112,12 @@ def test_create_fails_loudly_without_device_and_validates():
     bad = ok.default_config(N=21)          # beyond the fused kernels' horizon
     with pytest.raises(ok.KiteNmpcError):
         ok.BatchNMPC(p, bad, 4)
+    for i, lo, hi in ((13, -1.0, float("inf")), (14, -float("inf"), 3.0), (3, 1.0, -1.0), (5, float("nan"), 1.0)):
+        bad = ok.default_config()          # finite theta/thetadot bounds (not enforced) or a bad box: refused
+        bad.lbx[i], bad.ubx[i] = lo, hi
+        with pytest.raises(ok.KiteNmpcError) as e:
+            ok.BatchNMPC(p, bad, 4)
+        assert e.value.code == nmpc.KITE_EINVAL, i
     if not _gpu_present():
         with pytest.raises(ok.KiteNmpcError) as e:
             ok.BatchNMPC(p, ok.default_config(), 4)
