@@ -45,6 +45,7 @@ struct kite_nmpc_ctx {
     // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
+    double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20)
     // scratch for the model-level entry points
     double* scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -176,7 +177,7 @@ int ensure_scratch(kite_nmpc_ctx* ctx, size_t bytes) {
 void free_ctx(kite_nmpc_ctx* ctx) {
     double** bufs[] = {&ctx->X, &ctx->U, &ctx->x0, &ctx->AB, &ctx->DEF, &ctx->Hs, &ctx->hs,
                        &ctx->Cr, &ctx->cl, &ctx->cu, &ctx->hmax, &ctx->u0, &ctx->diag, &ctx->kkt,
-                       &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb};
+                       &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb, &ctx->wstep};
     for (double** p : bufs) if (*p) { (void)hipFree(*p); *p = nullptr; }
     if (ctx->status) { (void)hipFree(ctx->status); ctx->status = nullptr; }
     if (ctx->iters) { (void)hipFree(ctx->iters); ctx->iters = nullptr; }
@@ -209,7 +210,8 @@ int run_step(kite_nmpc_ctx* ctx) {
     if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
                                       ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
-                                      ctx->status, ctx->kkt, ctx->iters, ctx->order, ctx->order + B, s));
+                                      ctx->status, ctx->kkt, ctx->iters, ctx->order, ctx->order + B, ctx->wstep,
+                                      s));
     else
         HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
                                 ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters,
@@ -379,7 +381,7 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         {&ctx->hs, B * n}, {&ctx->Cr, B * N * n}, {&ctx->cl, B * N}, {&ctx->cu, B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
         {&ctx->Htl, ctx->tiled ? B * ntile * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
-        {&ctx->Hbb, ctx->tiled ? B * 4 : 1},
+        {&ctx->Hbb, ctx->tiled ? B * 4 : 1}, {&ctx->wstep, ctx->tiled ? B * n : 1},
     };
     for (const Alloc& a : allocs) {
         if (hipMalloc(a.p, a.count * sizeof(double)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }

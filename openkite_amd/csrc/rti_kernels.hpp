@@ -48,7 +48,7 @@ hipError_t launch_qp_tiled(const ModelConst& P, const RtiConst& C, int B, const 
                            const double* Hbb, const double* hs, const double* Cr, const double* cl,
                            const double* cu, const double* hmax, const double* AB, const double* DEF, double* X,
                            double* U, double* u0, double* diag, int32_t* status, double* kkt, int32_t* iters,
-                           const int32_t* order, int32_t* lazy, hipStream_t s);
+                           const int32_t* order, int32_t* lazy, double* wstep, hipStream_t s);
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
