@@ -45,7 +45,8 @@ struct kite_nmpc_ctx {
     // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
-    double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20)
+    double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
+                                   // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
     // scratch for the model-level entry points
     double* scratch = nullptr;
     size_t scratch_bytes = 0;
