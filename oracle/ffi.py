@@ -75,9 +75,10 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
 def cfg_vector(c: Dict) -> np.ndarray:
     v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
          *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
-         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4)]
+         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4), c.get("qp_form", 0),
+         c.get("soft_weight", 1e3), c.get("lm", 10.0)]
     a = np.array(v, dtype=np.float64)
-    assert a.size == 77
+    assert a.size == 80
     return a
 
 
@@ -109,7 +110,9 @@ def lib():
             "orc_build_qp": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
             "orc_qp_solve": (d, [i, i, dp, dp, dp, dp, dp, dp, i, dp]),
             "orc_prologue": (i, [dp, dp, i, i, dp, i, i, dp, dp, dp]),
-            "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i]),
+            "orc_msqp_solve": (d, [dp, dp, i, i, dp, dp, i, dp, ip]),
+            "orc_msqp_build": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
+            "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i, ip]),
             "orc_traj_cost": (d, [dp, i, dp, dp]),
             "orc_cheb_points": (None, [i, dp]),
             "orc_cheb_D": (None, [i, dp]),
@@ -238,21 +241,45 @@ def qp_solve(H, h, lb, ub, C, c, K):
     return w, kkt
 
 
+def msqp_solve(kp, cfgv, N, M, X, U, K):
+    """Multiple-shooting QP (qp_form 1) at the linearisation point (X, U) after
+    the prologue; returns (v, kkt, iterations), v = [dx_0 du_0 ... dx_N] scaled."""
+    nv = (N + 1) * 15 + N * 4
+    v = np.zeros(nv)
+    it = np.zeros(1, dtype=np.int32)
+    kkt = lib().orc_msqp_solve(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), int(K), _p(v),
+                               it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return v, kkt, int(it[0])
+
+
+def msqp_build(kp, cfgv, N, M, X, U):
+    """The multiple-shooting QP's data (scaled): dict of A, B, d, J, r, Rh, rho, lo, hi."""
+    nv = (N + 1) * 15 + N * 4
+    o = dict(A=np.zeros((N, 15, 15)), B=np.zeros((N, 15, 4)), d=np.zeros((N, 15)), J=np.zeros((N + 1, 4, 15)),
+             r=np.zeros((N + 1, 4)), Rh=np.zeros(4), rho=np.zeros((N, 4)), lo=np.zeros(nv), hi=np.zeros(nv))
+    lib().orc_msqp_build(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), *(_p(o[k]) for k in
+                         ("A", "B", "d", "J", "r", "Rh", "rho", "lo", "hi")))
+    return o
+
+
 def prologue(kp, cfgv, N, M, x0, X, U, warm, shift=1):
     X = _f64(X).copy(); U = _f64(U).copy(); x0o = np.zeros(15)
     st = lib().orc_prologue(_p(kp), _p(cfgv), N, M, _p(_f64(x0)), int(warm), int(shift), _p(X), _p(U), _p(x0o))
     return st, X, U, x0o
 
 
-def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0):
-    """Batched RTI step.  x0 (B,15); X (B,N+1,15) and U (B,N,4) updated in place."""
+def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0, iters=None):
+    """Batched RTI step.  x0 (B,15); X (B,N+1,15) and U (B,N,4) updated in place.
+    iters (optional int32 array of B): QP interior-point iterations per kite (the
+    condensed form counts the last re-solve only)."""
     B = x0.shape[0]
     assert X.shape == (B, N + 1, 15) and U.shape == (B, N, 4)
     assert X.dtype == np.float64 and U.dtype == np.float64 and X.flags["C_CONTIGUOUS"] and U.flags["C_CONTIGUOUS"]
     u0 = np.zeros((B, 4)); diag = np.zeros((B, 6)); status = np.zeros(B, dtype=np.int32)
+    ip = ctypes.POINTER(ctypes.c_int32)
     lib().orc_rti_step(_p(kp), _p(cfgv), N, M, K, B, int(warm), int(shift), _p(_f64(x0)), _p(X), _p(U),
-                       _p(u0), _p(diag), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-                       int(nthreads))
+                       _p(u0), _p(diag), status.ctypes.data_as(ip), int(nthreads),
+                       None if iters is None else iters.ctypes.data_as(ip))
     return u0, diag, status
 
 
