@@ -48,7 +48,8 @@ def parse(argv=None):
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--substeps", type=int, default=2)
     ap.add_argument("--qp-iters", type=int, default=16)
-    ap.add_argument("--qp-kernel", type=int, default=0, help="0 auto, 1 wave-scalar, 2 MFMA-tiled")
+    ap.add_argument("--qp-kernel", type=int, default=0,
+                    help="0 auto (= 3), 1 condensed wave-scalar, 2 condensed MFMA-tiled, 3 multiple-shooting Riccati")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--fp32-sens", action="store_true",
                     help="RK4 + sensitivities in fp32, QP fp64 (BASELINE configs[3] mixed precision)")
@@ -182,7 +183,7 @@ def pmc_traffic(kernel, cfg_tag):
             continue
         ks = d.get("kernels", {})
         for name in sorted(ks):
-            if name.split("<")[0] in (f"k_{kernel}_tiled", f"k_{kernel}_lds", f"k_{kernel}") and \
+            if name.split("<")[0] in (f"k_{kernel}_ric", f"k_{kernel}_tiled", f"k_{kernel}_lds", f"k_{kernel}") and \
                     "traffic_bytes" in ks[name]:
                 return ks[name]["traffic_bytes"], os.path.relpath(f, ROOT) + f" ({name})"
     return None, "no PMC summary of this configuration"
@@ -194,11 +195,60 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(args) -> int:
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def count_gpus(kfd_nodes=KFD_NODES, dev_dri="/dev/dri", env=None) -> int:
+    """GPUs this process may use, counted WITHOUT any HIP call (no torch.cuda,
+    no amdsmi fallback that initialises HIP): the KFD topology nodes with SIMDs
+    (CPU nodes have none) whose render node /dev/dri/renderD<minor> exists and
+    is accessible, capped by a *_VISIBLE_DEVICES list when one is set."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        nodes = sorted(os.listdir(kfd_nodes))
+    except OSError:
+        nodes = []
+    for d in nodes:
+        props = {}
+        try:
+            with open(os.path.join(kfd_nodes, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.strip().partition(" ")
+                    props[k] = v
+        except OSError:
+            continue
+        try:
+            if int(props.get("simd_count", "0")) <= 0:
+                continue
+            minor = int(props.get("drm_render_minor", "-1"))
+        except ValueError:
+            continue
+        rn = os.path.join(dev_dri, f"renderD{minor}")
+        if minor >= 0 and os.path.exists(rn) and os.access(rn, os.R_OK | os.W_OK):
+            n += 1
+    if not nodes:
+        # no readable KFD topology: the accessible render nodes (one per GPU)
+        try:
+            n = sum(1 for e in os.listdir(dev_dri) if e.startswith("renderD")
+                    and os.access(os.path.join(dev_dri, e), os.R_OK | os.W_OK))
+        except OSError:
+            n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None and v.strip() != "":
+            n = min(n, len([t for t in v.split(",") if t.strip() != ""]))
+    return n
+
+
+def launch_ranks(args, count=count_gpus, call=subprocess.call) -> int:
     """--gpus N without a launcher: start N ranks (one per GPU) as a child
-    torch.distributed.run, before this process touches any GPU."""
-    import torch
-    have = torch.cuda.device_count()          # does not initialise the GPU on this image
+    torch.distributed.run, before this process touches any GPU (an exec or a
+    fork after HIP initialisation is what this pool forbids)."""
+    if "torch" in sys.modules:
+        import torch
+        assert not torch.cuda.is_initialized(), "bench.py: HIP initialised before the ranks were started"
+    have = count()
     if have < args.gpus:
         print(f"bench.py: --gpus {args.gpus} requested but this node has {have} GPU(s)", file=sys.stderr)
         return 2
@@ -206,7 +256,7 @@ def launch_ranks(args) -> int:
            "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    return call(cmd, env=env)
 
 
 def main():
@@ -275,7 +325,8 @@ def main():
         # mean over every instance of every timed step (device-side running
         # sums restarted by timing_start), not just the last step
         mean_it = it_sum / float(B * args.steps)
-        fl = flops.rti(N, args.substeps, mean_it)
+        ric = args.qp_kernel in (0, 3)
+        fl = flops.rti_ric(N, args.substeps, mean_it) if ric else flops.rti(N, args.substeps, mean_it)
         kernels = ["prologue", "rk4_sens", "condense", "qp"]
         avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels}
         dom = max(kernels, key=lambda k: avg_ms[k])
@@ -283,7 +334,8 @@ def main():
         achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic(dom, run_config_tag(args))
-        roofline = dict(bound="mfma", achieved=round(achieved, 4), peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
+        roofline = dict(bound="fp64 (VALU+MFMA, latency-bound)", achieved=round(achieved, 4),
+                        peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic, kernel=dom,
                         note="fp64 compute roof (vector = matrix peak on gfx950); achieved = algorithmic flops "
                              "per launch (openkite_amd/flops.py) / mean launch time (HIP events on the step "
@@ -321,6 +373,12 @@ def main():
             "qp_mean_iterations": round(mean_it, 3),
             "qp_converged_frac": round(float(np.mean(kkt < 1e-8)), 5),
             "status_nan": int(np.sum(status & 1)),
+            "status_last_step": {name: int(np.sum((status & bit) != 0)) for name, bit in
+                                 (("nan", 1), ("qp_not_converged", 2), ("state_bound", 8), ("rejected", 32),
+                                  ("restart", 64))},
+            "qp": "multiple-shooting QP, Riccati IPM (k_qp_ric)" if ric else "condensed QP (k_qp_tiled / k_qp_lds / k_qp)",
+            "algorithmic_flops_per_launch": {("k_qp_ric" if ric else "qp"): fl["qp"] * B,
+                                             "k_rk4_sens2": fl["rk4_sens"] * B},
             "run_config": run_config_tag(args),
         }
         print(json.dumps(out), flush=True)

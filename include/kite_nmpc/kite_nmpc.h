@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 1
+#define KITE_NMPC_API_VERSION 2   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+                                      qp_kernel 3 (multiple-shooting QP, Riccati IPM) */
 
 /* ---- error codes ------------------------------------------------------ */
 #define KITE_OK        0
@@ -91,9 +92,14 @@ typedef struct kite_nmpc_config {
     int32_t shift;        /* 1: shift the warm start by one interval per step  */
     int32_t device;       /* HIP device ordinal                                 */
     int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
-    int32_t qp_kernel;    /* 0: auto (MFMA-tiled QP when N == 20 or 40), 1: wave-scalar LDS QP,
-                             2: MFMA-tiled (register tiles at N == 20, LDS tiles with
-                             4 waves per kite at N == 40; KITE_EINVAL otherwise) */
+    int32_t qp_kernel;    /* 0: auto (= 3), 1: condensed QP, wave-scalar LDS IPM,
+                             2: condensed QP, MFMA-tiled IPM (register tiles at N == 20, LDS
+                             tiles with 4 waves per kite at N == 40; KITE_EINVAL otherwise),
+                             3: multiple-shooting QP (every node state a variable, as the
+                             reference NLP kiteNMPF.cpp:145-160), Riccati IPM on MFMA tiles,
+                             soft state bounds (qp_soft_weight) and a Levenberg-Marquardt
+                             term (qp_lm).  1 and 2 enforce the state bounds of states 1..12
+                             as lazy rows. */
     int32_t delay_steps;  /* RK4 substeps of the delay-compensation prediction (4) */
     double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
     double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */
@@ -120,6 +126,11 @@ typedef struct kite_nmpc_config {
     int32_t sens_fp32;    /* 1: RK4 + forward sensitivities in fp32 (mixed precision,
                              BASELINE config 4); condensing, QP, expansion stay fp64 */
     int32_t reserved;
+    double qp_soft_weight; /* qp_kernel 3: exact-L1 weight of the state bounds in the reference's
+                              scaled units (1e3); the QP stays feasible when the linearised
+                              dynamics cannot meet the box over the horizon                   */
+    double qp_lm;          /* qp_kernel 3: Levenberg-Marquardt term lm/2 ||step||^2 on every QP
+                              variable, scaled units (10); leaves the RTI fixed point unchanged */
 } kite_nmpc_config;
 
 /* ---- diagnostics: msg/mpc_diagnostic.msg (filled at nmpf_node.cpp:191-204) */

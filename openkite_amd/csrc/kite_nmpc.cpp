@@ -5,6 +5,7 @@
 // CPU fallback: every numerical entry point runs on the GPU.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cctype>
 #include <chrono>
 #include <cmath>
@@ -44,6 +45,8 @@ struct kite_nmpc_ctx {
     // tiled-QP layout (N == 20, 40): H_aa lower tiles [B][NT(NT+1)/2][4][64] with
     // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
+    bool ric = false;              // multiple-shooting QP + Riccati IPM (qp_kernel 3): no condensing
+    kite::RicConst ricc;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
                                    // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
@@ -129,6 +132,51 @@ RtiConst make_rti_const(const kite_nmpc_config& c) {
     return r;
 }
 
+// Constants of the multiple-shooting QP (qp_ric.inc; oracle build_msqp):
+// per stage slot j (0..12 kite states, 13..15 T dE dR, 16 theta, 17 thetadot,
+// 18 Uv) its bound and scale, and the inequality rows per stage type.
+kite::RicConst make_ric_const(const kite_nmpc_config& c) {
+    kite::RicConst r;
+    std::memset(&r, 0, sizeof(r));
+    r.soft_w = c.qp_soft_weight;
+    r.lm = c.qp_lm;
+    r.hth = c.dt * c.Sx[13] / c.Sx[14];
+    r.g0 = 0.5 * c.dt * c.dt * c.Sx[13] / c.Su[3];
+    r.g1 = c.dt * c.Sx[14] / c.Su[3];
+    for (int a = 0; a < 3; ++a) {
+        r.sq[0][a] = std::sqrt(c.dt * c.Q[a]);
+        r.sq[1][a] = std::sqrt(c.Q[a]);
+    }
+    r.sw = std::sqrt(c.dt * c.W);
+    r.ctheta = 1.0 / c.Sx[13];
+    for (int q = 0; q < 4; ++q) r.Rh[q] = c.dt * c.R[q];
+    for (int j = 0; j < 20; ++j) { r.lb[j] = -INFINITY; r.ub[j] = INFINITY; r.sc[j] = 1.0; }
+    for (int i = 0; i < 13; ++i) { r.lb[i] = c.lbx[i]; r.ub[i] = c.ubx[i]; r.sc[i] = c.Sx[i]; }
+    for (int q = 0; q < 4; ++q) {
+        const int j = q < 3 ? 13 + q : 18;
+        r.lb[j] = c.lbu[q]; r.ub[j] = c.ubu[q]; r.sc[j] = c.Su[q];
+    }
+    r.lb[16] = -c.theta_flex; r.ub[16] = c.theta_flex; r.sc[16] = c.Sx[13];
+    r.lb[17] = -c.theta_flex; r.ub[17] = c.theta_flex; r.sc[17] = c.Sx[14];
+    int rw = 0, nC = 0;
+    for (int t = 0; t < 3; ++t) {
+        int row = 0, pairs = 0;
+        for (int j = 0; j < 20; ++j) {
+            const bool state = j < 13, ctrl = (j >= 13 && j < 16) || j == 18, theta = (j == 16 || j == 17);
+            const bool live = (state && t > 0) || (ctrl && t < 2) || (theta && t == 0);
+            r.rlo[t][j] = -1; r.rhi[t][j] = -1;
+            if (!live) continue;
+            if (std::isfinite(r.lb[j])) { r.rlo[t][j] = (int8_t)row++; pairs += state ? 2 : 1; }
+            if (std::isfinite(r.ub[j])) { r.rhi[t][j] = (int8_t)row++; pairs += state ? 2 : 1; }
+        }
+        rw = std::max(rw, row);
+        nC += pairs * (t == 1 ? c.N - 1 : 1);
+    }
+    r.RW = rw;
+    r.nC = nC;
+    return r;
+}
+
 int validate_config(const kite_nmpc_config& c) {
     if (c.N < 1 || c.N > KITE_NMAX) return KITE_EINVAL;
     if (c.M < 1 || c.M > 64) return KITE_EINVAL;
@@ -148,7 +196,9 @@ int validate_config(const kite_nmpc_config& c) {
     for (int i = 0; i < 3; ++i) if (!(c.Q[i] >= 0.0)) return KITE_EINVAL;
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
-    if (c.qp_kernel < 0 || c.qp_kernel > 2) return KITE_EINVAL;
+    if (c.qp_kernel < 0 || c.qp_kernel > 3) return KITE_EINVAL;
+    if (!(c.qp_soft_weight > 2.0 * 10.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;   // > 2 z0
+    if (!(c.qp_lm >= 0.0) || !std::isfinite(c.qp_lm)) return KITE_EINVAL;
     if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
     if (!(c.delay >= 0.0) || !std::isfinite(c.delay) || std::lround(c.delay / c.dt) > c.N) return KITE_EINVAL;
     if (c.delay > 0.0 && (c.delay_steps < 1 || c.delay_steps > 64)) return KITE_EINVAL;
@@ -202,13 +252,17 @@ int run_step(kite_nmpc_ctx* ctx) {
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, s));
     if (ev) HIP_TRY(hipEventRecord(ev[2], s));
-    HIP_TRY(kite::launch_condense(ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, ctx->Hs, ctx->hs, ctx->Cr,
-                                  ctx->cl, ctx->cu, ctx->hmax, ctx->tiled ? 1 : 0, ctx->Htl, ctx->Hab, ctx->Hbb,
-                                  s));
+    if (!ctx->ric)
+        HIP_TRY(kite::launch_condense(ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, ctx->Hs, ctx->hs, ctx->Cr,
+                                      ctx->cl, ctx->cu, ctx->hmax, ctx->tiled ? 1 : 0, ctx->Htl, ctx->Hab,
+                                      ctx->Hbb, s));
     // QP dispatch order from the previous step's iteration counts (ctx->iters[0, B))
     HIP_TRY(kite::launch_qp_order(ctx->rc, B, ctx->iters, ctx->order, ctx->order + B, s));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
-    if (ctx->tiled)
+    if (ctx->ric)
+        HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
+                                    ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order, s));
+    else if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
                                       ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
                                       ctx->status, ctx->kkt, ctx->iters, ctx->order, ctx->order + B, ctx->wstep,
@@ -351,6 +405,8 @@ void kite_nmpc_default_config(kite_nmpc_config* c) {
     c->path_q[0] = std::cos(pi / 8); c->path_q[1] = 0.0; c->path_q[2] = std::sin(pi / 8); c->path_q[3] = 0.0;
     c->theta_flex = 0.78;
     c->min_speed = 2.1;
+    c->qp_soft_weight = 1e3;
+    c->qp_lm = 10.0;
 }
 
 int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int32_t batch,
@@ -372,14 +428,20 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     const size_t B = (size_t)batch, N = (size_t)cfg->N, n = 4 * N + 2;
     const bool tiled_ok = kite::qp_tiled_supported(ctx->rc);
     if (cfg->qp_kernel == 2 && !tiled_ok) { delete ctx; return KITE_EINVAL; }
-    ctx->tiled = cfg->qp_kernel == 2 || (cfg->qp_kernel == 0 && tiled_ok);
+    ctx->ric = cfg->qp_kernel == 3 || cfg->qp_kernel == 0;
+    ctx->tiled = !ctx->ric && cfg->qp_kernel == 2;
+    if (ctx->ric) {
+        ctx->ricc = make_ric_const(*cfg);
+        if (kite::qp_ric_lds_bytes(ctx->rc, ctx->ricc) > 160 * 1024 - 1024) { delete ctx; return KITE_EINVAL; }
+    }
     const size_t na = 4 * N;
     const size_t ntile = (N / 4) * (N / 4 + 1) / 2;
     struct Alloc { double** p; size_t count; };
     const Alloc allocs[] = {
         {&ctx->X, B * (N + 1) * 15}, {&ctx->U, B * N * 4}, {&ctx->x0, B * 15},
-        {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13}, {&ctx->Hs, ctx->tiled ? 1 : B * n * n},
-        {&ctx->hs, B * n}, {&ctx->Cr, B * N * n}, {&ctx->cl, B * N}, {&ctx->cu, B * N},
+        {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13},
+        {&ctx->Hs, (ctx->tiled || ctx->ric) ? 1 : B * n * n}, {&ctx->hs, ctx->ric ? 1 : B * n},
+        {&ctx->Cr, ctx->ric ? 1 : B * N * n}, {&ctx->cl, ctx->ric ? 1 : B * N}, {&ctx->cu, ctx->ric ? 1 : B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
         {&ctx->Htl, ctx->tiled ? B * ntile * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
         {&ctx->Hbb, ctx->tiled ? B * 4 : 1}, {&ctx->wstep, ctx->tiled ? B * n : 1},
@@ -880,6 +942,7 @@ int kite_nmpc_qp_iteration_sum(kite_nmpc_ctx* ctx, int64_t* sum) {
 int kite_nmpc_get_qp(kite_nmpc_ctx* ctx, int32_t instance, double* H, double* h, double* C, double* cl,
                      double* cu) {
     if (!ctx || instance < 0 || instance >= ctx->B) return KITE_EINVAL;
+    if (ctx->ric) return KITE_ESTATE;      // the multiple-shooting QP is never condensed
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t N = ctx->cfg.N, n = 4 * N + 2, b = instance;
     hipStream_t s = ctx->stream;

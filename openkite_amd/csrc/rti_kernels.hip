@@ -2147,5 +2147,6 @@ hipError_t launch_closest_point(const RtiConst& C, int count, const double* pos,
 }
 
 #include "qp_tiled.inc"
+#include "qp_ric.inc"
 
 }  // namespace kite

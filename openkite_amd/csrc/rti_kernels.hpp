@@ -35,6 +35,28 @@ struct RtiConst {
     int sens_fp32, pad2_;   // 1: k_rk4_sens2 in fp32 (DualF2)
 };
 
+// Multiple-shooting QP + Riccati interior point (qp_ric.inc, oracle qp_form 1):
+// constants precomputed on the host from kite_nmpc_config.
+struct RicConst {
+    double soft_w;      // L1 weight of the soft state bounds (scaled units)
+    double lm;          // Levenberg-Marquardt term on every QP variable
+    double hth, g0, g1; // scaled theta dynamics: th' = th + hth thd + g0 Uv, thd' = thd + g1 Uv
+    double sq[2][3];    // path rows sqrt(w Q_a): [0] k < N (w = dt), [1] k = N (w = 1)
+    double sw;          // speed row sqrt(dt W)
+    double ctheta;      // Sx[6+a] / Sx13 factor of dP/dtheta in the theta column: 1 / Sx13
+    double Rh[4];       // control Hessian (scaled): dt R_c
+    double lb[20], ub[20], sc[20];   // per stage slot: bound and scale (see qp_ric.inc)
+    int RW;             // inequality rows per stage (LDS stride)
+    int nC;             // complementarity pairs per kite (rows + soft rows over all stages)
+    int8_t rlo[3][20], rhi[3][20];   // row of the lower / upper bound of slot j for stage
+                                     // type t (0: k = 0, 1: 0 < k < N, 2: k = N); -1 = none
+};
+bool qp_ric_supported(const RtiConst& C);
+size_t qp_ric_lds_bytes(const RtiConst& C, const RicConst& R);
+hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, int B, const double* AB, const double* DEF,
+                         double* X, double* U, double* u0, double* diag, int32_t* status, double* kkt,
+                         int32_t* iters, int32_t* iters_acc, const int32_t* order, hipStream_t s);
+
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
                            double* X, double* U, int32_t* status, hipStream_t s);
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,

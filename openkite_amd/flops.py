@@ -18,6 +18,20 @@ Per instance:
   qp       : per interior-point iteration, n = 4N+2, m = N:
              H w 2n^2, C w and C^T z 4mn, normal matrix n(n+1)/2 * (2m+1),
              Cholesky n^3/3, two solves 2 * (2n^2 + 4mn)
+  qp_ric   : the multiple-shooting QP (qp_kernel 3, no condensing), per
+             interior-point iteration and stage (nx = 15 states, nu = 4
+             controls, the kite block Z = [A | B] is 13 x 16):
+               factorisation  P Z for the kite and theta rows   2*15*13*16
+                              Z' (P Z), symmetric half            16*17/2*13*2
+                              theta border (W' P_bb W, M_xi,beta) 3*16*2 + 40
+                              4x4 Cholesky + L^-1 M_ux            30 + 15*16
+                              rank-4 update, symmetric half       15*16/2*4*2
+               two solves     backward Z'p 13*16*2 + S's 15*4*2 + L^-1 g 16
+                              forward  S x 15*4*2 + L^-T 16 + Z xi 13*16*2
+               adjoint        Z' lambda 13*16*2 (stationarity test)
+               elementwise    R_ROW flops per bound row: residual, Sigma and
+                              rhs, two step directions, two ratio tests,
+                              mu_aff, update (counted from qp_ric.inc)
 """
 from __future__ import annotations
 
@@ -56,5 +70,29 @@ def qp(N: int, iterations: float) -> float:
 
 def rti(N: int, M: int, mean_qp_iterations: float) -> dict:
     d = dict(rk4_sens=rk4_sens(N, M), condense=condense(N), qp=qp(N, mean_qp_iterations))
+    d["total"] = sum(d.values())
+    return d
+
+
+# ---- multiple-shooting QP (qp_kernel 3, openkite_amd/csrc/qp_ric.inc) --------
+RIC_FACT = 2 * 15 * 13 * 16 + 16 * 17 // 2 * 13 * 2 + (3 * 16 * 2 + 40) + (30 + 15 * 16) + 15 * 16 // 2 * 4 * 2
+RIC_SOLVE = (13 * 16 * 2 + 15 * 4 * 2 + 16) + (15 * 4 * 2 + 16 + 13 * 16 * 2)
+RIC_ADJ = 13 * 16 * 2
+R_ROW = 80           # per bound row and iteration, each quantity counted once: residual 8, Sigma + rhs 16,
+                     # affine direction 12 + ratio 4 + mu_aff 6, corrector rhs 10, direction 12 + ratio 4, update 8
+ROWS_PER_STAGE = 23  # node configuration: 8 control rows + 15 state rows (nmpf_node.cpp:45-63)
+
+
+def qp_ric_per_iteration(N: int, rows_per_stage: int = ROWS_PER_STAGE) -> float:
+    return N * (RIC_FACT + 2 * RIC_SOLVE + RIC_ADJ) + (N + 1) * rows_per_stage * R_ROW
+
+
+def qp_ric(N: int, iterations: float) -> float:
+    # start: forward simulation (Z xi per stage); final residual: one adjoint sweep
+    return iterations * qp_ric_per_iteration(N) + N * (13 * 16 * 2 + RIC_ADJ)
+
+
+def rti_ric(N: int, M: int, mean_qp_iterations: float) -> dict:
+    d = dict(rk4_sens=rk4_sens(N, M), condense=0.0, qp=qp_ric(N, mean_qp_iterations))
     d["total"] = sum(d.values())
     return d

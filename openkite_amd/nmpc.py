@@ -54,6 +54,7 @@ class NmpcConfig(ctypes.Structure):
         ("path_q", ctypes.c_double * 4), ("theta_flex", ctypes.c_double), ("min_speed", ctypes.c_double),
         ("delay", ctypes.c_double),
         ("sens_fp32", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("qp_soft_weight", ctypes.c_double), ("qp_lm", ctypes.c_double),
     ]
 
     def to_dict(self) -> dict:

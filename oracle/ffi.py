@@ -69,13 +69,16 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
         path_q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0],
         flex=0.78, min_speed=2.1,
         delay=0.0, delay_steps=4,     # node transport delay 0.1 s (nmpf_node.cpp:74); 0 = KiteNMPF alone
+        qp_form=1,                    # 1: multiple-shooting QP (the product default, qp_kernel 0/3);
+                                      # 0: condensed QP + lazy state rows (qp_kernel 1/2)
+        soft_weight=1e3, lm=10.0,     # kite_nmpc_default_config qp_soft_weight, qp_lm
     )
 
 
 def cfg_vector(c: Dict) -> np.ndarray:
     v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
          *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
-         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4), c.get("qp_form", 0),
+         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4), c.get("qp_form", 1),
          c.get("soft_weight", 1e3), c.get("lm", 10.0)]
     a = np.array(v, dtype=np.float64)
     assert a.size == 80

@@ -39,8 +39,8 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(ok.KiteParams) == 52 * 8
     assert ctypes.sizeof(ok.MpcDiagnostic) == 6 * 8
     # kite_nmpc_config: 8 int32 + 91 doubles + 2 int32
-    assert ctypes.sizeof(ok.NmpcConfig) == 10 * 4 + (1 + 3 + 4 + 1 + 15 + 4 + 15 + 15 + 4 + 4 + 1 + 2 + 4 + 2 + 1) * 8
-    assert ok.lib().kite_nmpc_api_version() == 1
+    assert ctypes.sizeof(ok.NmpcConfig) == 10 * 4 + (1 + 3 + 4 + 1 + 15 + 4 + 15 + 15 + 4 + 4 + 1 + 2 + 4 + 2 + 1 + 2) * 8
+    assert ok.lib().kite_nmpc_api_version() == 2
 
 
 def test_load_properties_matches_yaml_and_oracle():

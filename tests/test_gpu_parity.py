@@ -22,6 +22,11 @@ RTI_TOL = 1e-6      # RTI u0/traj/ctrl, relative to max(1,|oracle|) per array.
                     # so two correct fp64 solvers agree only to that envelope.
 
 
+def condensed_cfgv(Nh=N):
+    """Oracle configuration of the condensed QP (qp_kernel 1 / 2, qp_form 0)."""
+    return ffi.cfg_vector(dict(ffi.node_config(N=Nh), qp_form=0))
+
+
 def rel(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
     return np.abs(a - b).max() / max(1.0, np.abs(b).max())
@@ -116,10 +121,11 @@ def gpu_to_oracle_perm(N):
     return np.array(p)
 
 
-def test_condensed_qp_vs_oracle(kp, cfgv):
+def test_condensed_qp_vs_oracle(kp):
     B = 8
+    cfgv = condensed_cfgv()
     x0 = x0_batch(B)
-    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), B)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(qp_kernel=2), B)
     try:
         g.step(x0)
         perm = gpu_to_oracle_perm(N)
@@ -313,7 +319,7 @@ def test_full_batch_properties():
         g1.close(); g2.close()
 
 
-@pytest.mark.parametrize("qp_kernel", [1, 2])
+@pytest.mark.parametrize("qp_kernel", [1, 2, 3])
 def test_qp_iteration_sum_matches_per_step_counts(qp_kernel):
     """kite_nmpc_qp_iteration_sum (bench.py's FLOP count) = the per-step
     iteration counts of kite_nmpc_qp_stats summed over steps and instances,
@@ -338,9 +344,11 @@ def test_qp_iteration_sum_matches_per_step_counts(qp_kernel):
 
 
 @pytest.mark.parametrize("qp_kernel", [1, 2])
-def test_qp_kernels_vs_oracle(kp, cfgv, qp_kernel):
-    """Both QP kernels (1 = wave-scalar, 2 = MFMA-tiled) against the oracle."""
+def test_qp_kernels_vs_oracle(kp, qp_kernel):
+    """Both condensed-QP kernels (1 = wave-scalar, 2 = MFMA-tiled) against the
+    oracle's condensed QP (qp_form 0)."""
     B = 16
+    cfgv = condensed_cfgv()
     x = x0_batch(B, offset=2000)
     cfg = ok.default_config()
     cfg.qp_kernel = qp_kernel
@@ -385,7 +393,7 @@ def test_n40_qp_kernels_vs_oracle(kp, qp_kernel):
     LDS-tiled QP (2, k_qp_lds) against the oracle over 4 warm steps, plus the
     tiled H layout reassembled by get_qp."""
     B, Nh = 16, 40
-    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    cv = condensed_cfgv(Nh)
     x = x0_batch(B, offset=7000)
     cfg = ok.default_config(N=Nh)
     cfg.qp_kernel = qp_kernel

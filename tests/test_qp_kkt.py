@@ -118,8 +118,8 @@ def test_certificate_on_oracle_closed_loop(kp):
     """The certificate itself (CPU): it accepts the oracle's IPM solutions along
     3 closed-loop steps and rejects a perturbed solution."""
     N = 20
-    cfg = ok.default_config(N=N)
-    cv = ffi.cfg_vector(ffi.node_config(N=N))
+    cfg = ok.default_config(N=N, qp_kernel=2)
+    cv = ffi.cfg_vector(dict(ffi.node_config(N=N), qp_form=0))
     B = 4
     xs = ffi.synthetic_states(B, offset=8000)
     x = np.zeros((B, 15)); x[:, :13] = xs
@@ -147,11 +147,11 @@ def test_certificate_on_oracle_closed_loop(kp):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,qp_kernel", [(20, 2), (20, 1), (40, 0)])
+@pytest.mark.parametrize("N,qp_kernel", [(20, 2), (20, 1), (40, 2)])
 def test_gpu_qp_solution_satisfies_kkt(kp, N, qp_kernel):
     B = 16
     cfg = ok.default_config(N=N, qp_kernel=qp_kernel)
-    cv = ffi.cfg_vector(ffi.node_config(N=N))
+    cv = ffi.cfg_vector(dict(ffi.node_config(N=N), qp_form=0))
     xs = ffi.synthetic_states(B, offset=8000)
     x = np.zeros((B, 15)); x[:, :13] = xs
     for b in range(B):

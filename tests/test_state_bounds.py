@@ -22,6 +22,7 @@ RTI_TOL = 1e-6          # as tests/test_gpu_parity.py
 
 def tight_config(N):
     c = ffi.node_config(N=N)
+    c["qp_form"] = 0          # the lazy rows belong to the condensed QP (qp_kernel 1 / 2)
     c["lbx"][3:6] = [-W_BOUND] * 3
     c["ubx"][3:6] = [W_BOUND] * 3
     return c
@@ -43,7 +44,7 @@ def within_bound(X):
 def test_oracle_lazy_rows_enforce_tight_rate_bound(kp):
     N, B = 20, 64
     cv = ffi.cfg_vector(tight_config(N))
-    cd = ffi.cfg_vector(ffi.node_config(N=N))
+    cd = ffi.cfg_vector(dict(ffi.node_config(N=N), qp_form=0))
     x = x0_batch(B, cv, 11000)
     Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
     active = kept = 0

@@ -52,8 +52,11 @@ for k, d in out.items():
     d["write_bytes"] = d.get("WRITE_SIZE_bytes_raw", 0.0)
     d["traffic_bytes"] = d["read_bytes"] + d["write_bytes"]
 bench_config = None
+algo_flops = None
 try:                       # the bench line of the same session: which configuration was profiled
-    bench_config = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])["run_config"]
+    line = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    bench_config = line["run_config"]
+    algo_flops = line.get("algorithmic_flops_per_launch")
 except Exception:
     pass
 json.dump({"tag": tag,
@@ -72,6 +75,7 @@ if os.path.exists(sq_csv):
             per[k][int(r.get("Dispatch_Id") or r.get("Correlation_Id"))][r["Counter_Name"]] = float(r["Counter_Value"])
     sq = {}
     SIMDS = 256 * 4
+    XCDS = 8
     for k, disp in per.items():
         ids = sorted(disp)
         st = ids[WARMUP:] if len(ids) > WARMUP else ids
@@ -84,16 +88,26 @@ if os.path.exists(sq_csv):
             d["frac_active_inst_any"] = avg.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
             d["frac_active_valu"] = avg.get("SQ_ACTIVE_INST_VALU", 0.0) / wc
         if avg.get("GRBM_GUI_ACTIVE", 0.0) > 0:
-            # MfmaUtil as rocprofv3 derives it: MFMA-busy cycles over GPU-busy cycles x SIMDs
-            d["mfma_util"] = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (avg["GRBM_GUI_ACTIVE"] * SIMDS)
+            # MFMA-busy cycles over GPU-busy cycles x SIMDs.  GRBM_GUI_ACTIVE is
+            # summed over the 8 XCDs (MI355X_MICROARCH.md, GRBM row): one XCD's
+            # busy cycles are GRBM_GUI_ACTIVE / 8 (27.08 M / 8 over 1.44 ms =
+            # 2.35 GHz in the r02z trace), so the SIMD-cycle denominator is
+            # (GRBM_GUI_ACTIVE / 8) x 1024 SIMDs
+            d["gpu_busy_cycles_per_xcd"] = avg["GRBM_GUI_ACTIVE"] / XCDS
+            d["mfma_util"] = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (avg["GRBM_GUI_ACTIVE"] / XCDS * SIMDS)
         d["mfma_f64_flops"] = avg.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) * 512.0
+        alg = (algo_flops or {}).get(k)
+        if alg:
+            # executed MFMA flops (padding included) over the kernel's algorithmic flops per launch
+            d["algorithmic_flops"] = alg
+            d["mfma_executed_over_algorithmic"] = d["mfma_f64_flops"] / alg
         sq[k] = d
     json.dump({"tag": tag, "bench_config": bench_config,
                "command": "rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY "
                           "SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 "
                           "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -- python bench.py --steps 30 --warmup 3",
                "note": "per launch, steady-state launches; WAVE/WAIT/ACTIVE in quad-cycles summed over waves; "
-                       "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs) (rocprofv3's MfmaUtil); "
+                       "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); "
                        "mfma_f64_flops = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512",
                "kernels": sq}, open(os.path.join(prof, f"{tag}_sq_mfma.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
