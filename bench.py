@@ -325,7 +325,7 @@ def main():
         # mean over every instance of every timed step (device-side running
         # sums restarted by timing_start), not just the last step
         mean_it = it_sum / float(B * args.steps)
-        ric = args.qp_kernel in (0, 3)
+        ric = ok.resolve_qp_kernel(args.qp_kernel, N) == 3
         fl = flops.rti_ric(N, args.substeps, mean_it) if ric else flops.rti(N, args.substeps, mean_it)
         kernels = ["prologue", "rk4_sens", "condense", "qp"]
         avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels}

@@ -92,7 +92,7 @@ typedef struct kite_nmpc_config {
     int32_t shift;        /* 1: shift the warm start by one interval per step  */
     int32_t device;       /* HIP device ordinal                                 */
     int32_t timing;       /* 1: record per-kernel hipEvents (kite_nmpc_kernel_times) */
-    int32_t qp_kernel;    /* 0: auto (= 3), 1: condensed QP, wave-scalar LDS IPM,
+    int32_t qp_kernel;    /* 0: auto (2 at N == 20, else 3), 1: condensed QP, wave-scalar LDS IPM,
                              2: condensed QP, MFMA-tiled IPM (register tiles at N == 20, LDS
                              tiles with 4 waves per kite at N == 40; KITE_EINVAL otherwise),
                              3: multiple-shooting QP (every node state a variable, as the

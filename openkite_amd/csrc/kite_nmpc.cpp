@@ -47,6 +47,9 @@ struct kite_nmpc_ctx {
     bool tiled = false;
     bool ric = false;              // multiple-shooting QP + Riccati IPM (qp_kernel 3): no condensing
     kite::RicConst ricc;
+    // device copy of (rc, ricc) read by k_qp_ric; re-uploaded when the host copy changes
+    void* dconst = nullptr;
+    std::vector<unsigned char> dconst_host;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
                                    // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
@@ -158,21 +161,20 @@ kite::RicConst make_ric_const(const kite_nmpc_config& c) {
     }
     r.lb[16] = -c.theta_flex; r.ub[16] = c.theta_flex; r.sc[16] = c.Sx[13];
     r.lb[17] = -c.theta_flex; r.ub[17] = c.theta_flex; r.sc[17] = c.Sx[14];
-    int rw = 0, nC = 0;
+    int nC = 0;
     for (int t = 0; t < 3; ++t) {
-        int row = 0, pairs = 0;
+        int pairs = 0;
+        r.lomask[t] = 0; r.himask[t] = 0;
         for (int j = 0; j < 20; ++j) {
             const bool state = j < 13, ctrl = (j >= 13 && j < 16) || j == 18, theta = (j == 16 || j == 17);
-            const bool live = (state && t > 0) || (ctrl && t < 2) || (theta && t == 0);
-            r.rlo[t][j] = -1; r.rhi[t][j] = -1;
-            if (!live) continue;
-            if (std::isfinite(r.lb[j])) { r.rlo[t][j] = (int8_t)row++; pairs += state ? 2 : 1; }
-            if (std::isfinite(r.ub[j])) { r.rhi[t][j] = (int8_t)row++; pairs += state ? 2 : 1; }
+            const bool rows = (state && t > 0) || (ctrl && t < 2) || (theta && t == 0);
+            if (!rows) continue;
+            if (std::isfinite(r.lb[j])) { r.lomask[t] |= 1 << j; pairs += state ? 2 : 1; }
+            if (std::isfinite(r.ub[j])) { r.himask[t] |= 1 << j; pairs += state ? 2 : 1; }
+            if (std::isfinite(r.lb[j]) || std::isfinite(r.ub[j])) r.bslot[t][r.nb[t]++] = (int8_t)j;
         }
-        rw = std::max(rw, row);
         nC += pairs * (t == 1 ? c.N - 1 : 1);
     }
-    r.RW = rw;
     r.nC = nC;
     return r;
 }
@@ -230,6 +232,7 @@ void free_ctx(kite_nmpc_ctx* ctx) {
                        &ctx->Cr, &ctx->cl, &ctx->cu, &ctx->hmax, &ctx->u0, &ctx->diag, &ctx->kkt,
                        &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb, &ctx->wstep};
     for (double** p : bufs) if (*p) { (void)hipFree(*p); *p = nullptr; }
+    if (ctx->dconst) { (void)hipFree(ctx->dconst); ctx->dconst = nullptr; }
     if (ctx->status) { (void)hipFree(ctx->status); ctx->status = nullptr; }
     if (ctx->iters) { (void)hipFree(ctx->iters); ctx->iters = nullptr; }
     if (ctx->order) { (void)hipFree(ctx->order); ctx->order = nullptr; }
@@ -259,9 +262,21 @@ int run_step(kite_nmpc_ctx* ctx) {
     // QP dispatch order from the previous step's iteration counts (ctx->iters[0, B))
     HIP_TRY(kite::launch_qp_order(ctx->rc, B, ctx->iters, ctx->order, ctx->order + B, s));
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
-    if (ctx->ric)
-        HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
-                                    ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order, s));
+    if (ctx->ric) {
+        constexpr size_t roff = (sizeof(kite::RtiConst) + 255) / 256 * 256;
+        static_assert(roff + sizeof(kite::RicConst) <= 4096, "dconst holds both constant blocks");
+        unsigned char blob[roff + sizeof(kite::RicConst)] = {};
+        std::memcpy(blob, &ctx->rc, sizeof(kite::RtiConst));
+        std::memcpy(blob + roff, &ctx->ricc, sizeof(kite::RicConst));
+        if (ctx->dconst_host.size() != sizeof(blob) || std::memcmp(ctx->dconst_host.data(), blob, sizeof(blob))) {
+            ctx->dconst_host.assign(blob, blob + sizeof(blob));
+            HIP_TRY(hipMemcpyAsync(ctx->dconst, ctx->dconst_host.data(), sizeof(blob), hipMemcpyHostToDevice, s));
+        }
+        const auto* Cd = reinterpret_cast<const kite::RtiConst*>(ctx->dconst);
+        const auto* Rd = reinterpret_cast<const kite::RicConst*>(static_cast<const unsigned char*>(ctx->dconst) + roff);
+        HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, Cd, Rd, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0,
+                                    ctx->diag, ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order, s));
+    }
     else if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
                                       ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
@@ -428,8 +443,11 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     const size_t B = (size_t)batch, N = (size_t)cfg->N, n = 4 * N + 2;
     const bool tiled_ok = kite::qp_tiled_supported(ctx->rc);
     if (cfg->qp_kernel == 2 && !tiled_ok) { delete ctx; return KITE_EINVAL; }
-    ctx->ric = cfg->qp_kernel == 3 || cfg->qp_kernel == 0;
-    ctx->tiled = !ctx->ric && cfg->qp_kernel == 2;
+    // auto: the register-tiled condensed QP at N == 20 (fastest there, well
+    // conditioned over a 1 s horizon), the multiple-shooting QP otherwise
+    const int qk = cfg->qp_kernel != 0 ? cfg->qp_kernel : (cfg->N == 20 ? 2 : 3);
+    ctx->ric = qk == 3;
+    ctx->tiled = qk == 2;
     if (ctx->ric) {
         ctx->ricc = make_ric_const(*cfg);
         if (kite::qp_ric_lds_bytes(ctx->rc, ctx->ricc) > 160 * 1024 - 1024) { delete ctx; return KITE_EINVAL; }
@@ -452,7 +470,8 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     }
     if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->iters, 2 * B * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&ctx->order, (2 * (size_t)B + 1) * sizeof(int32_t)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
+        hipMalloc(&ctx->order, (2 * (size_t)B + 1) * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&ctx->dconst, 4096) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
     (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
     (void)hipMemset(ctx->iters, 0, 2 * B * sizeof(int32_t));   // [0, B): last step, [B, 2B): running sum
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -488,6 +507,7 @@ int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* 
     if (rc) return rc;
     ctx->cfg = c;
     ctx->rc = make_rti_const(c);
+    if (ctx->ric) ctx->ricc = make_ric_const(c);     // the QP's bounds
     return KITE_OK;
 }
 

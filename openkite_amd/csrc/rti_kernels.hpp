@@ -46,16 +46,19 @@ struct RicConst {
     double ctheta;      // Sx[6+a] / Sx13 factor of dP/dtheta in the theta column: 1 / Sx13
     double Rh[4];       // control Hessian (scaled): dt R_c
     double lb[20], ub[20], sc[20];   // per stage slot: bound and scale (see qp_ric.inc)
-    int RW;             // inequality rows per stage (LDS stride)
     int nC;             // complementarity pairs per kite (rows + soft rows over all stages)
-    int8_t rlo[3][20], rhi[3][20];   // row of the lower / upper bound of slot j for stage
-                                     // type t (0: k = 0, 1: 0 < k < N, 2: k = N); -1 = none
+    int lomask[3], himask[3];        // bit j: slot j has a lower / upper bound row at stage
+                                     // type t (0: k = 0, 1: 0 < k < N, 2: k = N)
+    int nb[3];                       // bounded slots per stage type ...
+    int8_t bslot[3][20];             // ... and their slot numbers
 };
 bool qp_ric_supported(const RtiConst& C);
 size_t qp_ric_lds_bytes(const RtiConst& C, const RicConst& R);
-hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, int B, const double* AB, const double* DEF,
-                         double* X, double* U, double* u0, double* diag, int32_t* status, double* kkt,
-                         int32_t* iters, int32_t* iters_acc, const int32_t* order, hipStream_t s);
+// C, R: host copies (launch geometry); Cd, Rd: the same constants in device memory
+hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, const RtiConst* Cd, const RicConst* Rd, int B,
+                         const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
+                         int32_t* status, double* kkt, int32_t* iters, int32_t* iters_acc, const int32_t* order,
+                         hipStream_t s);
 
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
                            double* X, double* U, int32_t* status, hipStream_t s);

@@ -198,6 +198,13 @@ def load_properties(path: str = DEFAULT_PARAMS) -> KiteParams:
     return p
 
 
+def resolve_qp_kernel(qp_kernel: int, N: int) -> int:
+    """The QP kernel a config selects (kite_nmpc_create): 0 (auto) is the
+    register-tiled condensed QP (2) at N == 20, the multiple-shooting QP (3)
+    otherwise."""
+    return qp_kernel if qp_kernel else (2 if N == 20 else 3)
+
+
 def default_config(**overrides) -> NmpcConfig:
     """The reference node's controller setup (nmpf_node.cpp:30-69) + RTI defaults."""
     c = NmpcConfig()

@@ -69,8 +69,9 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
         path_q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0],
         flex=0.78, min_speed=2.1,
         delay=0.0, delay_steps=4,     # node transport delay 0.1 s (nmpf_node.cpp:74); 0 = KiteNMPF alone
-        qp_form=1,                    # 1: multiple-shooting QP (the product default, qp_kernel 0/3);
-                                      # 0: condensed QP + lazy state rows (qp_kernel 1/2)
+        qp_form=0 if N == 20 else 1,  # the product's qp_kernel 0 (auto): N == 20 condensed QP + lazy
+                                      # state rows (qp_form 0, qp_kernel 2), otherwise the
+                                      # multiple-shooting QP (qp_form 1, qp_kernel 3)
         soft_weight=1e3, lm=10.0,     # kite_nmpc_default_config qp_soft_weight, qp_lm
     )
 

@@ -2,7 +2,10 @@
 the oracle (qp_form 1): B kites, a cold step and warm steps from identical
 inputs (the GPU restarts each step from the oracle's previous solution).
 
-  python tools/ric_check.py [N] [B] [steps]
+  python tools/ric_check.py [N] [B] [steps] [allbounds]
+
+allbounds = 1: finite (wide) bounds on every kite state, so that every
+interior node has 17 bounded variables (the NB = 13 register layout at N = 40).
 """
 import os
 import sys
@@ -19,12 +22,18 @@ steps = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 kp = ffi.load_params()
 c = ffi.node_config(N=N)
 c["qp_form"] = 1
+allb = len(sys.argv) > 4 and sys.argv[4] == "1"
+if allb:
+    c["lbx"] = [v if np.isfinite(v) or i >= 13 else -50.0 for i, v in enumerate(c["lbx"])]
+    c["ubx"] = [v if np.isfinite(v) or i >= 13 else 50.0 for i, v in enumerate(c["ubx"])]
 cv = ffi.cfg_vector(c)
 xs = ffi.synthetic_states(B)
 x = np.zeros((B, 15)); x[:, :13] = xs
 for b in range(B):
     x[b, 13] = ffi.closest_point(cv, xs[b, 6:9])
 g = ok.BatchNMPC(ok.load_properties(), ok.default_config(N=N, qp_kernel=3), B)
+if allb:
+    g.set_bounds(np.array(c["lbx"]), np.array(c["ubx"]))
 Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
 try:
     for step in range(steps):
