@@ -245,6 +245,16 @@ def qp_solve(H, h, lb, ub, C, c, K):
     return w, kkt
 
 
+def ms_trace():
+    """Per-iteration (r, mu, affine step, sigma, step) of the last msqp_solve on
+    this thread (debug aid)."""
+    L = lib()
+    buf = np.zeros(64 * 5)
+    L.orc_ms_trace.restype = ctypes.c_int
+    n = L.orc_ms_trace(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return buf[:5 * n].reshape(n, 5)
+
+
 def msqp_solve(kp, cfgv, N, M, X, U, K):
     """Multiple-shooting QP (qp_form 1) at the linearisation point (X, U) after
     the prologue; returns (v, kkt, iterations), v = [dx_0 du_0 ... dx_N] scaled."""

@@ -32,6 +32,26 @@ def rel(a, b):
     return np.abs(a - b).max() / max(1.0, np.abs(b).max())
 
 
+def rel_per_kite(a, b):
+    B = a.shape[0]
+    a, b = np.asarray(a, float).reshape(B, -1), np.asarray(b, float).reshape(B, -1)
+    return np.abs(a - b).max(1) / np.maximum(1.0, np.abs(b).max(1))
+
+
+MS_CAP_TOL = 1e-4   # multiple-shooting QP (qp_kernel 3): a QP that froze (residual
+                    # < 1e-10) on one side but ran to the cap K on the other (the
+                    # GPU's reduced-gradient residual floor is a few 1e-10 at
+                    # N = 40) -- measured differences <= 3e-6
+
+
+def assert_ms_rti(e, kkt_gpu, kkt_orc, where):
+    """RTI bar on every QP frozen on both sides, MS_CAP_TOL on the rest."""
+    frozen = (kkt_gpu < 1e-10) & (kkt_orc < 1e-10)
+    assert e[frozen].max(initial=0.0) < RTI_TOL, (where, np.sort(e[frozen])[-5:])
+    assert e[~frozen].max(initial=0.0) < MS_CAP_TOL, (where, np.sort(e[~frozen])[-5:])
+    return int(frozen.sum())
+
+
 @pytest.fixture(scope="module")
 def ctx1():
     c = ok.BatchNMPC(ok.load_properties(), ok.default_config(), 1)
@@ -379,8 +399,8 @@ def test_rti_horizons_vs_oracle(kp, Nh):
         for step in range(3):
             r = g.step(x)
             u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
-            e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
-            assert e < RTI_TOL, (Nh, step, e)
+            e = np.maximum(rel_per_kite(r["traj"], Xo), rel_per_kite(r["ctrl"], Uo))
+            assert_ms_rti(e, g.qp_stats()[0], diag[:, 5], (Nh, step))
             np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
             x = Xo[:, 1, :].copy()
     finally:
@@ -552,22 +572,30 @@ def test_config5_n40_fused_ekf_vs_oracle(kp):
     """BASELINE config 5: N = 40 with the fused EKF -> RTI sequence bench.py
     times (openkite_amd/fleet.py: 5 EKF propagation substeps of dt/5 under the
     applied control, update with the measured position + attitude, RTI from
-    the estimate), 256 kites x 4 closed-loop steps on torch's stream.  Every
-    step, the oracle repeats the sequence from the GPU loop's own state
-    before the step (estimate, covariance, measurement, applied control, warm
-    start), so each step is a parity check from identical inputs."""
+    the estimate), 256 kites x 12 closed-loop steps on torch's stream -- past
+    steps 5-9, where the condensed formulation's NaN / restart storms began
+    (profiles/r02z_oracle_n40_closed_loop_status.txt).  Every step, the oracle
+    repeats the sequence from the GPU loop's own state before the step
+    (estimate, covariance, measurement, applied control, warm start), so each
+    step is a parity check from identical inputs.  Per kite and step: status
+    words equal (NaN, restart, rejected, bound, min-speed, wrap; the not-
+    converged bit may differ only where the two residuals straddle its 1e-8
+    threshold), the RTI bar on every QP frozen on both sides, MS_CAP_TOL on
+    the rest; no NaN, no rejected step, no restart anywhere."""
     torch = pytest.importorskip("torch")
     from openkite_amd.fleet import FleetLoop, GpuStepper
-    B, Nh = 256, 40
+    B, Nh, steps = 256, 40, 12
     cv = ffi.cfg_vector(ffi.node_config(N=Nh))
     cfg = ok.default_config(N=Nh)
+    assert ok.resolve_qp_kernel(cfg.qp_kernel, Nh) == 3
     g = ok.BatchNMPC(ok.load_properties(), cfg, B)
     W, V, P0 = ok.ekf_default_covariances()
+    frozen_total = 0
     try:
         g.set_stream(torch.cuda.current_stream().cuda_stream)
         x0 = x0_batch(B, offset=11000)
         loop = FleetLoop(GpuStepper(g), torch.from_numpy(x0).cuda(), Nh, cfg.dt, ekf=True, covariances=(W, V, P0))
-        for step in range(4):
+        for step in range(steps):
             torch.cuda.synchronize()
             xe, P = loop.xe.cpu().numpy(), loop.P.cpu().numpy()
             u3, z, xin = loop.u0[:, :3].cpu().numpy(), loop.z.cpu().numpy(), loop.x0.cpu().numpy()
@@ -583,24 +611,18 @@ def test_config5_n40_fused_ekf_vs_oracle(kp):
             u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, xin, Xo, Uo, warm=int(step > 0), nthreads=0)
             tr = loop.traj.cpu().numpy()
             stg = loop.status.cpu().numpy()
-            same = (stg & 32) == (st & 32)
-            assert same.sum() >= B - 2
-            e = np.abs(tr - Xo).reshape(B, -1).max(1) / np.maximum(1.0, np.abs(Xo).reshape(B, -1).max(1))
-            # QPs that reached the 1e-10 freeze on both sides vs the oracle at the
-            # RTI bar; QPs stopped by the iteration cap K = 16 (no freeze, several
-            # per step at N = 40) are unconverged interior-point iterates, whose
-            # rounding-level input differences the ill-conditioned N = 40 QP
-            # (cond(H) ~ 3e11) amplifies -- measured: a kite stopped at residual
-            # 5.8e-10 after 16 iterations differs from the oracle's frozen
-            # solution by 5e-4, while a 1e-15 perturbation of H alone moves the
-            # oracle's own solution by 4e-5 -- held to 1e-2
-            conv = same & (loop.diag.cpu().numpy()[:, 5] < 1e-10) & (diag[:, 5] < 1e-10)
-            capped = same & ~conv
-            assert np.mean(e[conv] < RTI_TOL) >= 0.99 and e[conv].max() < 1e-4, (step, np.sort(e[conv])[-5:])
-            assert e[capped].max(initial=0.0) < 1e-2, (step, np.sort(e[capped])[-5:])
+            kg, ko = loop.diag.cpu().numpy()[:, 5], diag[:, 5]
+            np.testing.assert_array_equal(stg & ~2, st & ~2, err_msg=f"step {step}")
+            straddle = (np.minimum(kg, ko) < 1e-8) & (np.maximum(kg, ko) < 1e-7)
+            assert np.all(((stg & 2) == (st & 2)) | straddle), step
+            assert not np.any(stg & (1 | 32 | 64)), (step, np.unique(stg))
+            e = rel_per_kite(tr, Xo)
+            frozen_total += assert_ms_rti(e, kg, ko, step)
         assert np.all(np.isfinite(loop.traj.cpu().numpy()))
+        assert frozen_total >= 0.9 * B * steps, frozen_total
     finally:
         g.close()
+    print(f"config 5: {B} kites x {steps} steps, {frozen_total} QPs frozen on both sides")
 
 
 @pytest.mark.parametrize("fp32", [0, 1])
