@@ -275,7 +275,8 @@ int run_step(kite_nmpc_ctx* ctx) {
         const auto* Cd = reinterpret_cast<const kite::RtiConst*>(ctx->dconst);
         const auto* Rd = reinterpret_cast<const kite::RicConst*>(static_cast<const unsigned char*>(ctx->dconst) + roff);
         HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, Cd, Rd, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0,
-                                    ctx->diag, ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order, s));
+                                    ctx->diag, ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order,
+                                    ctx->Hs, s));
     }
     else if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
@@ -458,7 +459,8 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     const Alloc allocs[] = {
         {&ctx->X, B * (N + 1) * 15}, {&ctx->U, B * N * 4}, {&ctx->x0, B * 15},
         {&ctx->AB, B * N * 13 * 16}, {&ctx->DEF, B * N * 13},
-        {&ctx->Hs, (ctx->tiled || ctx->ric) ? 1 : B * n * n}, {&ctx->hs, ctx->ric ? 1 : B * n},
+        // ric: Hs is k_qp_ric's workspace (the factor rows S_k, qp_ric_ws_doubles per kite)
+        {&ctx->Hs, ctx->tiled ? 1 : (ctx->ric ? B * kite::qp_ric_ws_doubles(ctx->rc) : B * n * n)}, {&ctx->hs, ctx->ric ? 1 : B * n},
         {&ctx->Cr, ctx->ric ? 1 : B * N * n}, {&ctx->cl, ctx->ric ? 1 : B * N}, {&ctx->cu, ctx->ric ? 1 : B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
         {&ctx->Htl, ctx->tiled ? B * ntile * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},

@@ -54,11 +54,13 @@ struct RicConst {
 };
 bool qp_ric_supported(const RtiConst& C);
 size_t qp_ric_lds_bytes(const RtiConst& C, const RicConst& R);
-// C, R: host copies (launch geometry); Cd, Rd: the same constants in device memory
+// C, R: host copies (launch geometry); Cd, Rd: the same constants in device memory;
+// ws: workspace of qp_ric_ws_doubles(C) doubles per kite
+size_t qp_ric_ws_doubles(const RtiConst& C);
 hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, const RtiConst* Cd, const RicConst* Rd, int B,
                          const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
                          int32_t* status, double* kkt, int32_t* iters, int32_t* iters_acc, const int32_t* order,
-                         hipStream_t s);
+                         double* ws, hipStream_t s);
 
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
                            double* X, double* U, int32_t* status, hipStream_t s);
