@@ -149,39 +149,59 @@ __device__ __forceinline__ Dual2 datan2(Dual2 y, Dual2 x, Dual2 r2) {
     return mk2(atan2(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
 }
 
-// two fp32 tangents (mixed precision, config sens_fp32 = 1, k_rk4_sens2<DualF2>)
+// two fp32 tangents (mixed precision, config sens_fp32 = 1, k_rk4_sens2<DualF2>),
+// packed: the tangent pair is one float2 so every tangent update is ONE
+// v_pk_fma_f32 / v_pk_mul_f32 (two lanes of fp32 work per instruction)
+typedef float float2v __attribute__((ext_vector_type(2)));
 struct DualF2 {
-    float v, a, b;
+    float v;
+    union {
+        float2v t;
+        struct { float a, b; };
+    };
     DualF2() = default;
-    __host__ __device__ constexpr DualF2(double x) : v((float)x), a(0.0f), b(0.0f) {}
-    __host__ __device__ constexpr DualF2(float x, float ta, float tb) : v(x), a(ta), b(tb) {}
+    __host__ __device__ constexpr DualF2(double x) : v((float)x), t{0.0f, 0.0f} {}
+    __host__ __device__ constexpr DualF2(float x, float ta, float tb) : v(x), t{ta, tb} {}
+    __host__ __device__ constexpr DualF2(float x, float2v tt) : v(x), t(tt) {}
 };
+__device__ __forceinline__ float2v splat2(float f) { return float2v{f, f}; }
+__device__ __forceinline__ float2v fma2(float2v a, float2v b, float2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ DualF2 mkf2(float v, float2v t) { return DualF2(v, t); }
 __device__ __forceinline__ DualF2 mkf2(float v, float a, float b) { return DualF2(v, a, b); }
-__device__ __forceinline__ DualF2 operator+(DualF2 x, DualF2 y) { return mkf2(x.v + y.v, x.a + y.a, x.b + y.b); }
-__device__ __forceinline__ DualF2 operator-(DualF2 x, DualF2 y) { return mkf2(x.v - y.v, x.a - y.a, x.b - y.b); }
-__device__ __forceinline__ DualF2 operator-(DualF2 x) { return mkf2(-x.v, -x.a, -x.b); }
+__device__ __forceinline__ DualF2 operator+(DualF2 x, DualF2 y) { return mkf2(x.v + y.v, x.t + y.t); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x, DualF2 y) { return mkf2(x.v - y.v, x.t - y.t); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x) { return mkf2(-x.v, -x.t); }
 __device__ __forceinline__ DualF2 operator*(DualF2 x, DualF2 y) {
-    return mkf2(x.v * y.v, fmaf(x.a, y.v, x.v * y.a), fmaf(x.b, y.v, x.v * y.b));
+    return mkf2(x.v * y.v, fma2(x.t, splat2(y.v), x.v * y.t));
 }
-__device__ __forceinline__ DualF2 operator+(DualF2 x, double c) { return mkf2(x.v + (float)c, x.a, x.b); }
-__device__ __forceinline__ DualF2 operator+(double c, DualF2 x) { return mkf2(x.v + (float)c, x.a, x.b); }
-__device__ __forceinline__ DualF2 operator-(DualF2 x, double c) { return mkf2(x.v - (float)c, x.a, x.b); }
-__device__ __forceinline__ DualF2 operator-(double c, DualF2 x) { return mkf2((float)c - x.v, -x.a, -x.b); }
-__device__ __forceinline__ DualF2 operator*(DualF2 x, double c) { const float f = (float)c; return mkf2(x.v * f, x.a * f, x.b * f); }
-__device__ __forceinline__ DualF2 operator*(double c, DualF2 x) { const float f = (float)c; return mkf2(x.v * f, x.a * f, x.b * f); }
+__device__ __forceinline__ DualF2 operator+(DualF2 x, double c) { return mkf2(x.v + (float)c, x.t); }
+__device__ __forceinline__ DualF2 operator+(double c, DualF2 x) { return mkf2(x.v + (float)c, x.t); }
+__device__ __forceinline__ DualF2 operator-(DualF2 x, double c) { return mkf2(x.v - (float)c, x.t); }
+__device__ __forceinline__ DualF2 operator-(double c, DualF2 x) { return mkf2((float)c - x.v, -x.t); }
+__device__ __forceinline__ DualF2 operator*(DualF2 x, double c) { const float f = (float)c; return mkf2(x.v * f, x.t * f); }
+__device__ __forceinline__ DualF2 operator*(double c, DualF2 x) { const float f = (float)c; return mkf2(x.v * f, x.t * f); }
 __device__ __forceinline__ DualF2 operator/(DualF2 x, DualF2 y) {
     const float iy = 1.0f / y.v, q = x.v * iy;
-    return mkf2(q, (x.a - q * y.a) * iy, (x.b - q * y.b) * iy);
+    return mkf2(q, fma2(splat2(-q), y.t, x.t) * iy);
 }
-__device__ __forceinline__ DualF2 operator/(DualF2 x, double c) { const float ic = (float)(1.0 / c); return mkf2(x.v * ic, x.a * ic, x.b * ic); }
-__device__ __forceinline__ DualF2 rcp(DualF2 x) { const float r = 1.0f / x.v, nr2 = -r * r; return mkf2(r, x.a * nr2, x.b * nr2); }
+__device__ __forceinline__ DualF2 operator/(DualF2 x, double c) { const float ic = (float)(1.0 / c); return mkf2(x.v * ic, x.t * ic); }
+__device__ __forceinline__ DualF2 rcp(DualF2 x) { const float r = 1.0f / x.v, nr2 = -r * r; return mkf2(r, x.t * nr2); }
 __device__ __forceinline__ float val(DualF2 x) { return x.v; }
-__device__ __forceinline__ DualF2 dsqrt(DualF2 x) { const float s = sqrtf(x.v), h = 0.5f / s; return mkf2(s, x.a * h, x.b * h); }
-__device__ __forceinline__ DualF2 dexp(DualF2 x) { const float e = expf(x.v); return mkf2(e, x.a * e, x.b * e); }
-__device__ __forceinline__ DualF2 dasin(DualF2 x, DualF2 cosv) { const float ic = 1.0f / cosv.v; return mkf2(asinf(x.v), x.a * ic, x.b * ic); }
+__device__ __forceinline__ DualF2 dsqrt(DualF2 x) { const float s = sqrtf(x.v), h = 0.5f / s; return mkf2(s, x.t * h); }
+__device__ __forceinline__ DualF2 dexp(DualF2 x) { const float e = expf(x.v); return mkf2(e, x.t * e); }
+__device__ __forceinline__ DualF2 dasin(DualF2 x, DualF2 cosv) { const float ic = 1.0f / cosv.v; return mkf2(asinf(x.v), x.t * ic); }
 __device__ __forceinline__ DualF2 datan2(DualF2 y, DualF2 x, DualF2 r2) {
     const float ir = 1.0f / r2.v;
-    return mkf2(atan2f(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
+    return mkf2(atan2f(y.v, x.v), fma2(splat2(x.v), y.t, splat2(-y.v) * x.t) * ir);
+}
+// RK4 accumulation step acc + w k (rk4 kernels), packed for DualF2
+template <class DT, class ST>
+__device__ __forceinline__ DT rk_axpy(ST w, const DT& k, const DT& x) {
+    return DT(fma(w, k.v, x.v), fma(w, k.a, x.a), fma(w, k.b, x.b));
+}
+template <>
+__device__ __forceinline__ DualF2 rk_axpy<DualF2, float>(float w, const DualF2& k, const DualF2& x) {
+    return mkf2(fmaf(w, k.v, x.v), fma2(splat2(w), k.t, x.t));
 }
 
 template <class T> struct V3 { T x, y, z; };

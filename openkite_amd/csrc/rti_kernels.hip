@@ -238,8 +238,8 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
             const ST wn = (st < 2) ? ST(0.5) * hs : hs;
 #pragma unroll
             for (int i = 0; i < NK; ++i) {
-                acc[i] = DT(fma(wa, kv[i].v, acc[i].v), fma(wa, kv[i].a, acc[i].a), fma(wa, kv[i].b, acc[i].b));
-                xs[i] = DT(fma(wn, kv[i].v, x[i].v), fma(wn, kv[i].a, x[i].a), fma(wn, kv[i].b, x[i].b));
+                acc[i] = rk_axpy<DT, ST>(wa, kv[i], acc[i]);
+                xs[i] = rk_axpy<DT, ST>(wn, kv[i], x[i]);
             }
         }
 #pragma unroll
