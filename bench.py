@@ -171,10 +171,11 @@ def run_config_tag(args):
                 fp32_sens=bool(args.fp32_sens), ekf=bool(args.ekf), qp_kernel=args.qp_kernel)
 
 
-def pmc_traffic(kernel, cfg_tag):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<round>_pmc_hbm.json, tools/pmc_summary.py) whose recorded bench
-    configuration is this run's; None if no profile matches."""
+def pmc_traffic(names, cfg_tag):
+    """HBM bytes per launch of the kernel this run launches (one of `names`)
+    from the newest committed PMC summary (profiles/<round>_pmc_hbm.json,
+    tools/pmc_summary.py) whose recorded bench configuration is this run's;
+    None if no profile matches."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
     for f in reversed(files):
@@ -183,10 +184,17 @@ def pmc_traffic(kernel, cfg_tag):
             continue
         ks = d.get("kernels", {})
         for name in sorted(ks):
-            if name.split("<")[0] in (f"k_{kernel}_ric", f"k_{kernel}_tiled", f"k_{kernel}_lds", f"k_{kernel}") and \
-                    "traffic_bytes" in ks[name]:
+            if name.split("<")[0] in names and "traffic_bytes" in ks[name]:
                 return ks[name]["traffic_bytes"], os.path.relpath(f, ROOT) + f" ({name})"
     return None, "no PMC summary of this configuration"
+
+
+def dominant_kernel_names(dom, qp_kernel):
+    """rocprofv3 names of the kernel(s) behind the HIP-event phase `dom`."""
+    if dom != "qp":
+        return {"prologue": ("k_prologue",), "rk4_sens": ("k_rk4_sens2",),
+                "condense": ("k_condense20", "k_condense")}.get(dom, (f"k_{dom}",))
+    return {3: ("k_qp_ric",), 2: ("k_qp_tiled", "k_qp_lds"), 1: ("k_qp",)}[qp_kernel]
 
 
 def free_port():
@@ -333,13 +341,18 @@ def main():
         dom_flops = fl.get(dom, 0.0) * B
         achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
-        traffic, tsrc = pmc_traffic(dom, run_config_tag(args))
-        roofline = dict(bound="fp64 (VALU+MFMA, latency-bound)", achieved=round(achieved, 4),
+        qk = ok.resolve_qp_kernel(args.qp_kernel, N)
+        traffic, tsrc = pmc_traffic(dominant_kernel_names(dom, qk), run_config_tag(args))
+        # "mfma": the fp64 compute roof (the dense fp64 MFMA and vector peaks are
+        # both 78.6 TFLOP/s on gfx950); the kernel itself is bound by the latency
+        # of its dependent chains at one wave per SIMD, not by either pipe
+        roofline = dict(bound="mfma", achieved=round(achieved, 4),
                         peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
                         frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic, kernel=dom,
-                        note="fp64 compute roof (vector = matrix peak on gfx950); achieved = algorithmic flops "
-                             "per launch (openkite_amd/flops.py) / mean launch time (HIP events on the step "
-                             f"stream); traffic = HBM bytes per launch from {tsrc}")
+                        note="fp64 compute roof (dense fp64 MFMA = vector peak on gfx950); the kernel is "
+                             "latency-bound (dependent VALU/MFMA/LDS chains at 1 wave/SIMD); achieved = "
+                             "algorithmic flops per launch (openkite_amd/flops.py) / mean launch time (HIP "
+                             f"events on the step stream); traffic = HBM bytes per launch from {tsrc}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, x0_host, args.cpu_seconds)
