@@ -31,6 +31,12 @@
 
 #include "kite_nmpc.h"
 
+// Facade version (compile-time): 2 = getStats() returns kite_amd::Dict (a
+// string map with "return_status"; version 1 returned the status string),
+// getOptimalControl() is 4 x (N+1) as the reference's (version 1: 4 x N),
+// getPathFunction() and the C ABI's kite_nmpc_path_eval exist.
+#define KITE_NMPF_FACADE_VERSION 2
+
 namespace kite_amd {
 
 class KiteNmpcError : public std::runtime_error {
