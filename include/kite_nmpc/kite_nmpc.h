@@ -100,7 +100,7 @@ typedef struct kite_nmpc_config {
                              soft state bounds (qp_soft_weight) and a Levenberg-Marquardt
                              term (qp_lm).  1 and 2 enforce the state bounds of states 1..12
                              as lazy rows. */
-    int32_t delay_steps;  /* RK4 substeps of the delay-compensation prediction (4) */
+    int32_t delay_steps;  /* RK4 substeps of the delay-compensation prediction (16) */
     double dt;            /* interval length [s] (0.05 -> tf = 1 s at N = 20)  */
     double Q[3];          /* path weights  (kiteNMPF.cpp:32)                   */
     double R[4];          /* control weights (kiteNMPF.cpp:33)                 */
@@ -118,7 +118,8 @@ typedef struct kite_nmpc_config {
     double delay;         /* transport-delay compensation of the ROS node, fused into
                              the step (nmpf_node.cpp:206-221): on warm steps the kite
                              part of x0 is predicted over `delay` s under the previous
-                             u(t0) (RK4, delay_steps substeps; the node used CVODES)
+                             u(t0) (RK4, delay_steps substeps; the node used CVODES,
+                             abstol 1e-4: 16 substeps stay within 2e-5)
                              and theta, thetadot are taken from the previous trajectory
                              at node round(delay/dt).  0 = off: KiteNMPF semantics, the
                              caller passes the predicted state (default).  The node

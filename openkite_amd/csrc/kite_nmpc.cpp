@@ -391,7 +391,7 @@ void kite_nmpc_default_config(kite_nmpc_config* c) {
     std::memset(c, 0, sizeof(*c));
     const double inf = INFINITY, pi = M_PI;
     c->N = 20; c->M = 2; c->qp_iters = 16; c->shift = 1; c->device = 0; c->timing = 0;
-    c->delay = 0.0; c->delay_steps = 4;
+    c->delay = 0.0; c->delay_steps = 16;
     c->sens_fp32 = 0;
     c->dt = 0.05;
     const double Q[3] = {1e3, 1e3, 1e4};

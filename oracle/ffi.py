@@ -68,7 +68,7 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
         path_R=2.65, path_alt=0.0,
         path_q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0],
         flex=0.78, min_speed=2.1,
-        delay=0.0, delay_steps=4,     # node transport delay 0.1 s (nmpf_node.cpp:74); 0 = KiteNMPF alone
+        delay=0.0, delay_steps=16,    # node transport delay 0.1 s (nmpf_node.cpp:74); 0 = KiteNMPF alone
         qp_form=0 if N == 20 else 1,  # the product's qp_kernel 0 (auto): N == 20 condensed QP + lazy
                                       # state rows (qp_form 0, qp_kernel 2), otherwise the
                                       # multiple-shooting QP (qp_form 1, qp_kernel 3)
@@ -79,7 +79,7 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
 def cfg_vector(c: Dict) -> np.ndarray:
     v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
          *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
-         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 4), c.get("qp_form", 1),
+         c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 16), c.get("qp_form", 1),
          c.get("soft_weight", 1e3), c.get("lm", 10.0)]
     a = np.array(v, dtype=np.float64)
     assert a.size == 80

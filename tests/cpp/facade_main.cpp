@@ -13,7 +13,7 @@
 //   publish_trajectory (:140-188): getOptimalTrajetory + getPathFunction per
 //     column.
 // The delay prediction (the node's CVODES ODESolver, :75-84, :218) is RK4 on
-// the GPU here (kite_nmpc_predict, 0.1 s, 4 substeps); the plant is the plan's
+// the GPU here (kite_nmpc_predict, 0.1 s, 16 substeps); the plant is the plan's
 // own prediction at t0 + dt.  Prints one JSON line per control step.
 // Usage: facade_main <params.yaml> <steps> x0[0..12]
 #include <cmath>
@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
                 for (int i = 0; i < 13; ++i) x15[i] = kite_state[i];
                 for (int j = 0; j < 3; ++j) u4[j] = control[j];
                 kite_amd::kite_check(kite_nmpc_predict(controller.context(), 1, x15.data(), u4.data(),
-                                                       transport_delay, 4, xp.data()), "predict");
+                                                       transport_delay, 16, xp.data()), "predict");
                 for (int i = 0; i < 13; ++i) aug[i] = xp[i];
                 aug[13] = opt_traj[(size_t)(cols - 3) * 15 + 13];                      // column size2 - 3 (:220)
                 aug[14] = opt_traj[(size_t)(cols - 3) * 15 + 14];

@@ -61,7 +61,7 @@ def test_facade_node_sequence_matches_python_binding(tmp_path):
                 aug = np.r_[kite_state, g.closest_point(kite_state[6:9].reshape(1, 3), np.zeros(1))[0], 0.0]
                 prev = "none"
             else:
-                xp = g.predict(np.r_[kite_state, 0.0, 0.0].reshape(1, 15), np.r_[control, 0.0].reshape(1, 4), 0.1, 4)[0]
+                xp = g.predict(np.r_[kite_state, 0.0, 0.0].reshape(1, 15), np.r_[control, 0.0].reshape(1, 4), 0.1, 16)[0]
                 aug = np.r_[xp[:13], traj[2, 13:15]]          # column N-2 of the reversed order = node 2
                 prev = ok.nmpc._ReturnStatus(status).return_status
             aug[0] = max(aug[0], 2.1)

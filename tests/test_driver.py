@@ -44,7 +44,7 @@ def test_driver_matches_python_loop(tmp_path):
     steps = [r for r in recs if r["type"] == "step"]
     assert len(steps) == S and all(r["nan"] == 0 for r in steps)
 
-    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(delay=0.1, delay_steps=4), B)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(delay=0.1, delay_steps=16), B)
     try:
         plant = x13.copy()
         theta = g.closest_point(plant[:, 6:9], np.zeros(B))
@@ -94,7 +94,7 @@ def test_driver_matches_oracle_closed_loop(tmp_path, kp):
     recs = [json.loads(l) for l in out.strip().splitlines()]
     diag = {(r["step"], r["kite"]): r for r in recs if r["type"] == "mpc_diagnostic"}
     c = ffi.node_config()
-    c["delay"], c["delay_steps"] = 0.1, 4
+    c["delay"], c["delay_steps"] = 0.1, 16
     cv = ffi.cfg_vector(c)
     N = c["N"]
     Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))

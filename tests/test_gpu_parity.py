@@ -213,10 +213,10 @@ def test_delay_compensation_vs_oracle(kp):
     default, nmpf_node.cpp:74): 5 closed-loop steps of 16 kites vs the oracle."""
     B = 16
     c = ffi.node_config()
-    c["delay"], c["delay_steps"] = 0.1, 4
+    c["delay"], c["delay_steps"] = 0.1, 16
     cv = ffi.cfg_vector(c)
     x = x0_batch(B, offset=4000)
-    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(delay=0.1, delay_steps=4), B)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(delay=0.1, delay_steps=16), B)
     Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
     try:
         for step in range(5):

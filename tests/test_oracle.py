@@ -218,7 +218,7 @@ def test_delay_compensation_prologue(kp):
     theta/thetadot from the previous trajectory at node round(0.1/0.05) = 2."""
     N, M = 20, 2
     c = ffi.node_config()
-    c["delay"], c["delay_steps"] = 0.1, 4
+    c["delay"], c["delay_steps"] = 0.1, 16
     cv = ffi.cfg_vector(c)
     x0 = np.zeros(15)
     x0[:13] = ffi.synthetic_states(1, offset=5)[0]
