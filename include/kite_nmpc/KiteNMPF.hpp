@@ -34,8 +34,9 @@
 // Facade version (compile-time): 2 = getStats() returns kite_amd::Dict (a
 // string map with "return_status"; version 1 returned the status string),
 // getOptimalControl() is 4 x (N+1) as the reference's (version 1: 4 x N),
-// getPathFunction() and the C ABI's kite_nmpc_path_eval exist.
-#define KITE_NMPF_FACADE_VERSION 2
+// getPathFunction() and the C ABI's kite_nmpc_path_eval exist; 3 = arbitrary
+// closed paths (FourierPath, the KiteNMPF(params, path) constructor, setPath).
+#define KITE_NMPF_FACADE_VERSION 3
 
 namespace kite_amd {
 
@@ -64,6 +65,17 @@ inline kite_params LoadProperties(const std::string& yaml_path) {
     return p;
 }
 
+// The path argument of KiteNMPF(kite, path) (kiteNMPF.h:14), which takes any
+// casadi::Function theta -> R^3: a closed curve as a truncated Fourier series
+// per axis, rotated by q as the node rotates its circle (nmpf_node.cpp:30-40).
+// coef is 3 x (2K+1) row-major: axis a = x, y, z holds [c0, a1, b1, ..., aK, bK]
+// of p_a(theta) = c0 + sum_k a_k cos(k theta) + b_k sin(k theta), K <= 8.
+struct FourierPath {
+    int harmonics = 0;
+    std::vector<double> coef;
+    double q[4] = {1.0, 0.0, 0.0, 0.0};
+};
+
 class KiteNMPF {
 public:
     // KiteNMPF(shared_ptr<KiteDynamics>, path) (kiteNMPF.h:14): the dynamics are the
@@ -72,6 +84,23 @@ public:
         kite_nmpc_default_config(&cfg_);
         cfg_.N = N;
         cfg_.dt = dt;
+    }
+    // ... or any closed path
+    KiteNMPF(const kite_params& params, const FourierPath& path, int N = 20, double dt = 0.05)
+        : KiteNMPF(params, N, dt) {
+        setPath(path);
+    }
+    // the reference declares setPath(SX) without defining it (kiteNMPF.h:36); here it
+    // sets the path of the next createNLP()
+    void setPath(const FourierPath& path) {
+        const int K = path.harmonics;
+        if (K < 1 || K > KITE_PATH_MAX_HARMONICS || path.coef.size() != (size_t)3 * (2 * K + 1))
+            throw std::invalid_argument("setPath: coef must hold 3 x (2K+1) values, 1 <= K <= 8");
+        std::memset(cfg_.path_fourier, 0, sizeof(cfg_.path_fourier));
+        for (int a = 0; a < 3; ++a)
+            for (int j = 0; j < 2 * K + 1; ++j) cfg_.path_fourier[a][j] = path.coef[(size_t)a * (2 * K + 1) + j];
+        cfg_.path_harmonics = K;
+        for (int i = 0; i < 4; ++i) cfg_.path_q[i] = path.q[i];
     }
     KiteNMPF(const kite_params& params, const kite_nmpc_config& cfg) : params_(params), cfg_(cfg) {}
     ~KiteNMPF() { kite_nmpc_destroy(ctx_); }
@@ -150,7 +179,7 @@ public:
         return Dict{{"return_status", rs}, {"status_bits", std::to_string(status_)}};
     }
     // getPathFunction() (kiteNMPF.h:46): P(theta) of the configured path
-    // (the rotated circle of nmpf_node.cpp:30-40), evaluated on the host
+    // (the rotated circle of nmpf_node.cpp:30-40 or the FourierPath), evaluated on the host
     std::function<std::vector<double>(double)> getPathFunction() const {
         const kite_nmpc_config cfg = cfg_;
         return [cfg](double theta) {

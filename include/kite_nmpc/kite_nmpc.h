@@ -35,8 +35,11 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 2   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
-                                      qp_kernel 3 (multiple-shooting QP, Riccati IPM) */
+#define KITE_NMPC_API_VERSION 3   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+                                      qp_kernel 3 (multiple-shooting QP, Riccati IPM);
+                                   3: kite_nmpc_config gained path_harmonics, path_fourier
+                                      (arbitrary closed paths); delay_steps default 16 */
+#define KITE_PATH_MAX_HARMONICS 8 /* Fourier path: harmonics per axis              */
 
 /* ---- error codes ------------------------------------------------------ */
 #define KITE_OK        0
@@ -110,7 +113,8 @@ typedef struct kite_nmpc_config {
                                  13, 14 (theta, thetadot) are not bounded    */
     double lbu[4], ubu[4];    /* control bounds (nmpf_node.cpp:45-47)          */
     double vref;          /* physical path speed (setReferenceVelocity, nmpf_node.cpp:68) */
-    double path_radius;   /* P(theta) = rot(q)[R cos, R sin, alt] (nmpf_node.cpp:30-40) */
+    double path_radius;   /* P(theta) = rot(q)[R cos, R sin, alt] (nmpf_node.cpp:30-40)
+                             when path_harmonics == 0 (see path_fourier)             */
     double path_altitude;
     double path_q[4];     /* (w,x,y,z); P = vec(q^-1 (x) p (x) q)               */
     double theta_flex;    /* +- relaxation of theta, thetadot at t0 (kiteNMPF.cpp:226) */
@@ -132,6 +136,18 @@ typedef struct kite_nmpc_config {
                               dynamics cannot meet the box over the horizon                   */
     double qp_lm;          /* qp_kernel 3: Levenberg-Marquardt term lm/2 ||step||^2 on every QP
                               variable, scaled units (10); leaves the RTI fixed point unchanged */
+    /* Arbitrary closed path (KiteNMPF(kite, path), kiteNMPF.h:14, takes any
+     * casadi::Function theta -> R^3): with path_harmonics = K in 1..8 the
+     * unrotated curve is the truncated Fourier series
+     *   p_a(theta) = F[a][0] + sum_{k=1..K} F[a][2k-1] cos(k theta) + F[a][2k] sin(k theta)
+     * per axis a = x, y, z, and P(theta) = vec(q^-1 (x) [0, p] (x) q) with path_q
+     * as for the circle (path_radius / path_altitude are then unused).  The
+     * circle is K = 1, F[0][1] = F[1][2] = R, F[2][0] = alt.  0 (default): the
+     * circle.  Every path evaluation of the step (closest point, residuals,
+     * diagnostics, kite_nmpc_path_eval) uses it.                               */
+    int32_t path_harmonics;
+    int32_t reserved2;
+    double path_fourier[3][2 * KITE_PATH_MAX_HARMONICS + 1];
 } kite_nmpc_config;
 
 /* ---- diagnostics: msg/mpc_diagnostic.msg (filled at nmpf_node.cpp:191-204) */
@@ -182,7 +198,8 @@ int kite_nmpc_closest_point(kite_nmpc_ctx* ctx, int32_t count, const double* pos
                             const double* guess, double* theta_out);
 /* getPathFunction (kiteNMPF.h:46; the path built at nmpf_node.cpp:30-40 and
  * evaluated per trajectory node for /opt_traj at nmpf_node.cpp:177-183):
- * P(theta) = vec(q^-1 (x) [0, R cos, R sin, alt] (x) q) and dP/dtheta for
+ * P(theta) = vec(q^-1 (x) [0, p(theta)] (x) q) (the circle p = [R cos, R sin,
+ * alt] or the Fourier curve of path_harmonics) and dP/dtheta for
  * `count` angles (count x 3 each; dP3 may be NULL).  Host arithmetic on the
  * configuration only (no context, no GPU): a visualisation helper of the
  * node, not part of the RTI step.                                           */

@@ -26,7 +26,9 @@ __device__ __forceinline__ void colloc_path(const CollocConst& C, double th, dou
     const double qw = C.pq[0];
     const V3<double> qu{C.pq[1], C.pq[2], C.pq[3]};
     const double ww_uu = qw * qw - dot3(qu, qu);
-    const V3<double> p = rot_body(qw, qu, ww_uu, V3<double>{C.path_R * c, C.path_R * s, C.path_alt});
+    double pc[3], dpc[3];
+    path_curve(C.path_K, C.path_R, C.path_alt, C.pF, c, s, pc, dpc);
+    const V3<double> p = rot_body(qw, qu, ww_uu, V3<double>{pc[0], pc[1], pc[2]});
     P[0] = p.x; P[1] = p.y; P[2] = p.z;
 }
 

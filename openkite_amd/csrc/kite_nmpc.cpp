@@ -128,6 +128,10 @@ RtiConst make_rti_const(const kite_nmpc_config& c) {
     r.min_speed = c.min_speed;
     r.path_R = c.path_radius; r.path_alt = c.path_altitude;
     for (int i = 0; i < 4; ++i) r.pq[i] = c.path_q[i];
+    r.path_K = c.path_harmonics;
+    static_assert(KITE_PATH_NC == 2 * KITE_PATH_MAX_HARMONICS + 1, "path coefficient layout");
+    for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < KITE_PATH_NC; ++j) r.pF[a][j] = c.path_harmonics ? c.path_fourier[a][j] : 0.0;
     r.delay = c.delay;
     r.delay_steps = c.delay_steps;
     r.delay_node = (int)std::lround(c.delay / c.dt);
@@ -204,6 +208,10 @@ int validate_config(const kite_nmpc_config& c) {
     if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
     if (!(c.delay >= 0.0) || !std::isfinite(c.delay) || std::lround(c.delay / c.dt) > c.N) return KITE_EINVAL;
     if (c.delay > 0.0 && (c.delay_steps < 1 || c.delay_steps > 64)) return KITE_EINVAL;
+    if (c.path_harmonics < 0 || c.path_harmonics > KITE_PATH_MAX_HARMONICS) return KITE_EINVAL;
+    for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < 2 * c.path_harmonics + 1; ++j)
+            if (!std::isfinite(c.path_fourier[a][j])) return KITE_EINVAL;
     return KITE_OK;
 }
 
@@ -878,10 +886,13 @@ int kite_nmpc_path_eval(const kite_nmpc_config* cfg, int32_t count, const double
         out[1] = ww_uu * vy + 2.0 * ud * uy - 2.0 * w * cy;
         out[2] = ww_uu * vz + 2.0 * ud * uz - 2.0 * w * cz;
     };
+    if (cfg->path_harmonics < 0 || cfg->path_harmonics > KITE_PATH_MAX_HARMONICS) return KITE_EINVAL;
     for (int32_t i = 0; i < count; ++i) {
         const double s = std::sin(theta[i]), c = std::cos(theta[i]);
-        rot(cfg->path_radius * c, cfg->path_radius * s, cfg->path_altitude, P3 + 3 * (size_t)i);
-        if (dP3) rot(-cfg->path_radius * s, cfg->path_radius * c, 0.0, dP3 + 3 * (size_t)i);
+        double p[3], dp[3];
+        kite::path_curve(cfg->path_harmonics, cfg->path_radius, cfg->path_altitude, cfg->path_fourier, c, s, p, dp);
+        rot(p[0], p[1], p[2], P3 + 3 * (size_t)i);
+        if (dP3) rot(dp[0], dp[1], dp[2], dP3 + 3 * (size_t)i);
     }
     return KITE_OK;
 }

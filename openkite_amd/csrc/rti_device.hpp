@@ -120,16 +120,18 @@ __device__ __forceinline__ int wave_or(int v) {
     return wave_max((double)v) != 0.0 ? 1 : 0;
 }
 
-// Path P(theta) = q_r^-1 (x) [0, R cos, R sin, alt] (x) q_r and dP/dtheta
-// (nmpf_node.cpp:30-40).
+// Path P(theta) = q_r^-1 (x) [0, p(theta)] (x) q_r and dP/dtheta
+// (nmpf_node.cpp:30-40; p: the circle or the Fourier curve, kite_path.hpp).
 __device__ __forceinline__ void path_eval(const RtiConst& C, double th, double P[3], double dP[3]) {
     double s, c;
     sincos(th, &s, &c);
+    double pc[3], dpc[3];
+    path_curve(C.path_K, C.path_R, C.path_alt, C.pF, c, s, pc, dpc);
     const double qw = C.pq[0];
     const V3<double> qu{C.pq[1], C.pq[2], C.pq[3]};
     const double ww_uu = qw * qw - dot3(qu, qu);
-    V3<double> p = rot_body(qw, qu, ww_uu, V3<double>{C.path_R * c, C.path_R * s, C.path_alt});
-    V3<double> dp = rot_body(qw, qu, ww_uu, V3<double>{-C.path_R * s, C.path_R * c, 0.0});
+    V3<double> p = rot_body(qw, qu, ww_uu, V3<double>{pc[0], pc[1], pc[2]});
+    V3<double> dp = rot_body(qw, qu, ww_uu, V3<double>{dpc[0], dpc[1], dpc[2]});
     P[0] = p.x; P[1] = p.y; P[2] = p.z;
     dP[0] = dp.x; dP[1] = dp.y; dP[2] = dp.z;
 }

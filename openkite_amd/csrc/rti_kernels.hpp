@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "kite_model.hpp"
+#include "kite_path.hpp"
 
 // Largest horizon the fused condense/QP kernels are built for (LDS budget of
 // the wave-per-instance QP).  n = 4N+2 <= 82 decision variables.
@@ -33,6 +34,8 @@ struct RtiConst {
     double delay;       // delay compensation [s] (0 = off)
     int delay_steps, delay_node;
     int sens_fp32, pad2_;   // 1: k_rk4_sens2 in fp32 (DualF2)
+    int path_K, pad3_;      // 0: circle (path_R, path_alt); 1..8: Fourier path pF (kite_path.hpp)
+    double pF[3][KITE_PATH_NC];
 };
 
 // Multiple-shooting QP + Riccati interior point (qp_ric.inc, oracle qp_form 1):
@@ -103,6 +106,8 @@ struct CollocConst {
     double Q[3], R[4], W, vref;
     double Sx[15], Su[4], iSx[15], iSu[4];
     double path_R, path_alt, pq[4];
+    int path_K, pad_;
+    double pF[3][KITE_PATH_NC];
 };
 // tab = CompDiff (nodes x nodes, row-major) followed by the node weights (nodes)
 hipError_t launch_colloc(const ModelConst& P, const CollocConst& C, int count, const double* tab, const double* z,

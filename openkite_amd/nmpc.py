@@ -41,6 +41,10 @@ class KiteParams(ctypes.Structure):
         return np.array([getattr(self, f) for f in _PARAM_FIELDS], dtype=np.float64)
 
 
+PATH_HMAX = 8                      # KITE_PATH_MAX_HARMONICS
+PATH_NC = 2 * PATH_HMAX + 1
+
+
 class NmpcConfig(ctypes.Structure):
     _fields_ = [
         ("N", ctypes.c_int32), ("M", ctypes.c_int32), ("qp_iters", ctypes.c_int32), ("shift", ctypes.c_int32),
@@ -55,7 +59,26 @@ class NmpcConfig(ctypes.Structure):
         ("delay", ctypes.c_double),
         ("sens_fp32", ctypes.c_int32), ("reserved", ctypes.c_int32),
         ("qp_soft_weight", ctypes.c_double), ("qp_lm", ctypes.c_double),
+        ("path_harmonics", ctypes.c_int32), ("reserved2", ctypes.c_int32),
+        ("path_fourier", ctypes.c_double * (3 * PATH_NC)),   # [3][2 * 8 + 1], row-major
     ]
+
+    def set_fourier_path(self, coef, q=None) -> None:
+        """Arbitrary closed path (KiteNMPF(kite, path), kiteNMPF.h:14): coef is
+        (3, 2K + 1) per axis [c0, a1, b1, ..., aK, bK] of the unrotated curve
+        p_a(theta) = c0 + sum_k a_k cos(k theta) + b_k sin(k theta), K <= 8;
+        P = rot(q) p as for the circle (q None: keep path_q)."""
+        c = np.asarray(coef, dtype=np.float64)
+        if c.ndim != 2 or c.shape[0] != 3 or c.shape[1] % 2 != 1 or not 3 <= c.shape[1] <= PATH_NC:
+            raise ValueError("coef must be (3, 2K+1) with 1 <= K <= %d" % PATH_HMAX)
+        F = np.zeros((3, PATH_NC))
+        F[:, :c.shape[1]] = c
+        self.path_harmonics = (c.shape[1] - 1) // 2
+        for i, v in enumerate(F.reshape(-1)):
+            self.path_fourier[i] = v
+        if q is not None:
+            for i in range(4):
+                self.path_q[i] = q[i]
 
     def to_dict(self) -> dict:
         d = {}
@@ -524,11 +547,18 @@ class KiteNMPF:
 
     def setPath(self, radius: float, altitude: float = 0.0, q=(1.0, 0.0, 0.0, 0.0)):
         """The reference declares setPath(SX) but never defines it (kiteNMPF.h:36);
-        here the path family is the rotated circle of nmpf_node.cpp:30-40."""
+        the rotated circle of nmpf_node.cpp:30-40."""
         self._cfg.path_radius = radius
         self._cfg.path_altitude = altitude
         for i in range(4):
             self._cfg.path_q[i] = q[i]
+        self._cfg.path_harmonics = 0
+        self._impl = None
+
+    def setPathFourier(self, coef, q=(1.0, 0.0, 0.0, 0.0)):
+        """Any closed path (the path Function of KiteNMPF's ctor, kiteNMPF.h:14)
+        as a rotated Fourier curve, see NmpcConfig.set_fourier_path."""
+        self._cfg.set_fourier_path(coef, q)
         self._impl = None
 
     def _set(self, name, v):

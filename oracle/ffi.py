@@ -80,9 +80,12 @@ def cfg_vector(c: Dict) -> np.ndarray:
     v = [c["dt"], *c["Q"], *c["R"], c["W"], *c["Sx"], *c["Su"], *c["lbx"], *c["ubx"],
          *c["lbu"], *c["ubu"], c["vref"], c["path_R"], c["path_alt"], *c["path_q"],
          c["flex"], c["min_speed"], c.get("delay", 0.0), c.get("delay_steps", 16), c.get("qp_form", 1),
-         c.get("soft_weight", 1e3), c.get("lm", 10.0)]
-    a = np.array(v, dtype=np.float64)
-    assert a.size == 80
+         c.get("soft_weight", 1e3), c.get("lm", 10.0), c.get("path_K", 0)]
+    F = np.zeros((3, 17))
+    if c.get("path_K", 0):
+        F[:] = np.asarray(c["path_fourier"], dtype=np.float64).reshape(3, 17)
+    a = np.concatenate([np.array(v, dtype=np.float64), F.reshape(-1)])
+    assert a.size == 132
     return a
 
 

@@ -7,6 +7,7 @@ import ctypes
 import math
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -38,9 +39,23 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     assert ctypes.sizeof(ok.KiteParams) == 52 * 8
     assert ctypes.sizeof(ok.MpcDiagnostic) == 6 * 8
-    # kite_nmpc_config: 8 int32 + 91 doubles + 2 int32
-    assert ctypes.sizeof(ok.NmpcConfig) == 10 * 4 + (1 + 3 + 4 + 1 + 15 + 4 + 15 + 15 + 4 + 4 + 1 + 2 + 4 + 2 + 1 + 2) * 8
-    assert ok.lib().kite_nmpc_api_version() == 2
+    # kite_nmpc_config: 8 int32 + 91 doubles + 2 int32 + 2 int32 + 51 doubles (API 3: Fourier path)
+    assert ctypes.sizeof(ok.NmpcConfig) == 12 * 4 + (1 + 3 + 4 + 1 + 15 + 4 + 15 + 15 + 4 + 4 + 1 + 2 + 4 + 2 + 1 + 2 + 51) * 8
+    assert ok.lib().kite_nmpc_api_version() == 3
+
+
+def test_config_layout_matches_c_compiler(tmp_path):
+    """sizeof / offsetof of kite_nmpc_config from a C compiler == the ctypes mirror."""
+    src = tmp_path / "lay.c"
+    fields = [f for f, _ in ok.NmpcConfig._fields_]
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kite_nmpc/kite_nmpc.h"\nint main(void){'
+                   + 'printf("%zu\\n", sizeof(kite_nmpc_config));'
+                   + "".join(f'printf("%zu\\n", offsetof(kite_nmpc_config, {f}));' for f in fields) + "return 0;}")
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ok.nmpc.REPO, "include"), "-o", str(exe), str(src)], check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(ok.NmpcConfig)
+    assert out[1:] == [getattr(ok.NmpcConfig, f).offset for f in fields]
 
 
 def test_load_properties_matches_yaml_and_oracle():

@@ -81,3 +81,22 @@ def test_facade_node_sequence_matches_python_binding(tmp_path):
             kite_state = traj[1, :13].copy()
     finally:
         g.close()
+
+
+def test_facade_fourier_path(tmp_path):
+    """KiteNMPF(params, FourierPath) -> getPathFunction() equals the C ABI's
+    path evaluator on the same Fourier path (the reference's KiteNMPF takes any
+    path Function, kiteNMPF.h:14)."""
+    from test_path import fourier_path, product_config
+    exe = str(tmp_path / "facade_path")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "cpp", "facade_path.cpp"), "-L", LIBDIR, "-lkite_nmpc",
+                    f"-Wl,-rpath,{LIBDIR}", "-o", exe], check=True)
+    F = fourier_path()
+    cfg = product_config(F)
+    q = list(cfg.path_q)
+    args = [repr(float(v)) for v in F.reshape(-1)] + [repr(float(v)) for v in q] + [ok.nmpc.DEFAULT_PARAMS]
+    out = subprocess.run([exe] + args, check=True, capture_output=True, text=True).stdout.split("\n")
+    rows = np.array([[float(t) for t in l.split()] for l in out if l.strip()])
+    P, _ = ok.path_eval(cfg, rows[:, 0])
+    np.testing.assert_array_equal(rows[:, 1:], P)

@@ -214,7 +214,7 @@ def test_qp_sensitivity_envelope(kp, cfgv):
 
 def test_delay_compensation_prologue(kp):
     """Delay compensation (nmpf_node.cpp:206-221) in the oracle prologue: kite
-    state predicted over 0.1 s under the previous u(t0) with 4 RK4 substeps,
+    state predicted over 0.1 s under the previous u(t0) with 16 RK4 substeps,
     theta/thetadot from the previous trajectory at node round(0.1/0.05) = 2."""
     N, M = 20, 2
     c = ffi.node_config()
@@ -228,7 +228,7 @@ def test_delay_compensation_prologue(kp):
     U[0, :3] = [0.12, 0.01, -0.02]
     st2, X2, U2, x0p = ffi.prologue(kp, cv, N, M, x0, X, U, warm=1)
     up = np.array([0.12, 0.01, -0.02, 0.0])
-    pred = ffi.rk4(kp, x0, up, 0.025, 4)
+    pred = ffi.rk4(kp, x0, up, 0.1 / 16, 16)
     np.testing.assert_array_equal(x0p[:13], pred[:13])
     assert x0p[13] == X[2, 13] and x0p[14] == X[2, 14]
     np.testing.assert_array_equal(X2[0], x0p)

@@ -1,0 +1,178 @@
+"""Arbitrary closed paths (VERDICT r02 missing #4).
+
+The reference controller takes any path Function theta -> R^3
+(KiteNMPF(kite, path), kiteNMPF.h:14; the node passes the rotated circle of
+nmpf_node.cpp:30-40, kite_control_test.cpp:455-465 builds another circle).
+Here a path is the rotated circle or a rotated truncated Fourier curve
+(kite_nmpc_config.path_harmonics / path_fourier, K <= 8 harmonics per axis).
+
+CPU: kite_nmpc_path_eval (host arithmetic of the product library) against the
+oracle's path and finite differences; the K = 1 Fourier form of the node's
+circle reproduces the circle.  GPU (marked): closest point and closed-loop RTI
+steps on a three-harmonic path against the oracle, at N = 20 (condensed QP)
+and N = 40 (multiple-shooting QP).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import openkite_amd as ok
+from oracle import ffi
+
+R_NODE = 2.65
+
+
+def fourier_path():
+    """A non-circular closed path near the node's circle: x = R cos + 0.25 cos 2t,
+    y = R sin - 0.2 sin 3t, z = 0.1 + 0.4 sin 2t (then the node's rotation)."""
+    F = np.zeros((3, 7))
+    F[0, 1] = R_NODE; F[0, 3] = 0.25
+    F[1, 2] = R_NODE; F[1, 6] = -0.2
+    F[2, 0] = 0.1; F[2, 4] = 0.4
+    return F
+
+
+def circle_as_fourier():
+    F = np.zeros((3, 3))
+    F[0, 1] = R_NODE; F[1, 2] = R_NODE
+    return F
+
+
+def product_config(F, **kw):
+    c = ok.default_config(**kw)
+    c.set_fourier_path(F)
+    return c
+
+
+def oracle_config(F, **kw):
+    F17 = np.zeros((3, 17)); F17[:, :F.shape[1]] = F
+    return dict(ffi.node_config(**kw), path_K=(F.shape[1] - 1) // 2, path_fourier=F17)
+
+
+def test_path_eval_fourier_matches_oracle_and_derivative():
+    F = fourier_path()
+    c = product_config(F)
+    cv = ffi.cfg_vector(oracle_config(F))
+    th = np.linspace(-7.0, 7.0, 301)
+    P, dP = ok.path_eval(c, th)
+    for i, t in enumerate(th):
+        Po, dPo = ffi.path(cv, t)
+        np.testing.assert_allclose(P[i], Po, rtol=0, atol=1e-14)
+        np.testing.assert_allclose(dP[i], dPo, rtol=0, atol=1e-14)
+    # the unrotated curve, rotated by the node's quaternion (nmpf_node.cpp:35-39)
+    q = np.array(c.path_q)
+    w, u = q[0], q[1:]
+    def rot(v):
+        return (w * w - u @ u) * v + 2 * (u @ v) * u - 2 * w * np.cross(u, v)
+    for i, t in enumerate(th[::10]):
+        p = np.array([F[a, 0] + sum(F[a, 2 * k - 1] * math.cos(k * t) + F[a, 2 * k] * math.sin(k * t)
+                                    for k in range(1, 4)) for a in range(3)])
+        np.testing.assert_allclose(P[i * 10], rot(p), rtol=0, atol=1e-13)
+    h = 1e-6
+    Pp, _ = ok.path_eval(c, th + h)
+    Pm, _ = ok.path_eval(c, th - h)
+    np.testing.assert_allclose((Pp - Pm) / (2 * h), dP, rtol=0, atol=1e-8)
+
+
+def test_circle_as_fourier_equals_circle():
+    c0 = ok.default_config()
+    c1 = product_config(circle_as_fourier())
+    th = np.linspace(-4.0, 4.0, 97)
+    P0, dP0 = ok.path_eval(c0, th)
+    P1, dP1 = ok.path_eval(c1, th)
+    np.testing.assert_array_equal(P0, P1)
+    np.testing.assert_array_equal(dP0, dP1)
+
+
+def test_invalid_fourier_paths_refused():
+    c = ok.default_config()
+    c.path_harmonics = 9
+    with pytest.raises(RuntimeError):
+        ok.path_eval(c, [0.0])
+    with pytest.raises(ValueError):
+        c.set_fourier_path(np.zeros((3, 4)))
+    with pytest.raises(ValueError):
+        c.set_fourier_path(np.zeros((3, 19)))
+
+
+def test_oracle_closed_loop_on_fourier_path():
+    """The oracle's RTI on the three-harmonic path behaves as on the node's
+    circle: finite, no NaN / restart, and the scaled path error of this
+    synthetic loop (the plant is the plan's own prediction) stays within the
+    circle's envelope (measured over 30 steps: circle <= 1.31, this path <= 1.34)."""
+    N, M, K, B = 20, 2, 16, 8
+    cv = ffi.cfg_vector(oracle_config(fourier_path(), N=N))
+    x = x0_on_path(cv, B)
+    X = np.zeros((B, N + 1, 15)); U = np.zeros((B, N, 4))
+    errs = []
+    for step in range(8):
+        _, diag, st = ffi.rti_step(ffi.load_params(), cv, N, M, K, x, X, U, warm=int(step > 0))
+        assert np.all(np.isfinite(X)) and not np.any(st & (1 | 64)), st
+        errs.append(diag[:, 0].mean())
+        x = X[:, 1, :].copy()
+    assert max(errs) < 1.5, errs
+
+
+def x0_on_path(cv, B, offset=0):
+    xs = ffi.synthetic_states(B, offset=offset)
+    x = np.zeros((B, 15)); x[:, :13] = xs
+    for b in range(B):
+        x[b, 13] = ffi.closest_point(cv, xs[b, 6:9])
+    return x
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+@pytest.mark.gpu
+def test_gpu_closest_point_fourier_path_vs_oracle():
+    F = fourier_path()
+    cv = ffi.cfg_vector(oracle_config(F))
+    g = ok.BatchNMPC(ok.load_properties(), product_config(F), 1)
+    try:
+        rng = np.random.default_rng(5)
+        pos = rng.normal(size=(64, 3)) * 2.0
+        guess = rng.uniform(-3, 3, 64)
+        th = g.closest_point(pos, guess)
+    finally:
+        g.close()
+    ref = np.array([ffi.closest_point(cv, pos[i], guess[i]) for i in range(64)])
+    np.testing.assert_allclose(th, ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Nh", [20, 40])
+def test_gpu_rti_fourier_path_vs_oracle(kp, Nh):
+    """Closed-loop RTI steps on the three-harmonic path, GPU vs oracle with the
+    same inputs each step: N = 20 (condensed QP, k_qp_tiled) at the RTI bar on
+    every array; N = 40 (multiple-shooting QP, k_qp_ric) at the RTI bar on every
+    QP frozen on both sides; status words equal."""
+    from test_gpu_parity import RTI_TOL, assert_ms_rti, rel_per_kite
+    B, M, K = 16, 2, 16
+    F = fourier_path()
+    oc = oracle_config(F, N=Nh)
+    if Nh == 20:
+        oc["qp_form"] = 0
+    cv = ffi.cfg_vector(oc)
+    x = x0_on_path(cv, B, offset=3000)
+    g = ok.BatchNMPC(ok.load_properties(), product_config(F, N=Nh), B)
+    Xo = np.zeros((B, Nh + 1, 15)); Uo = np.zeros((B, Nh, 4))
+    try:
+        for step in range(5):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
+            if Nh == 20:
+                e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+                assert e < RTI_TOL, (step, e)
+            else:
+                e = np.maximum(rel_per_kite(r["traj"], Xo), rel_per_kite(r["ctrl"], Uo))
+                assert_ms_rti(e, g.qp_stats()[0], diag[:, 5], (Nh, step))
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            np.testing.assert_allclose(r["diag"][:, :5], diag[:, :5], rtol=1e-6, atol=1e-9)
+            assert np.all(np.isfinite(r["traj"]))
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
