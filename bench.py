@@ -49,7 +49,7 @@ def parse(argv=None):
     ap.add_argument("--substeps", type=int, default=2)
     ap.add_argument("--qp-iters", type=int, default=16)
     ap.add_argument("--qp-kernel", type=int, default=0,
-                    help="0 auto (= 3), 1 condensed wave-scalar, 2 condensed MFMA-tiled, 3 multiple-shooting Riccati")
+                    help="0 auto (2 at N = 20, else 3), 1 condensed wave-scalar, 2 condensed MFMA-tiled, 3 multiple-shooting Riccati")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--fp32-sens", action="store_true",
                     help="RK4 + sensitivities in fp32, QP fp64 (BASELINE configs[3] mixed precision)")
@@ -287,7 +287,11 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under a launcher (torch.distributed.run sets WORLD_SIZE) the ranks always
+    # join an RCCL group -- also at world 1, so the collective path (barrier,
+    # publish all-gather, max over ranks) runs on a one-GPU box too
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     B, N = args.batch, args.horizon
@@ -301,14 +305,14 @@ def main():
     offset, count = shard(world * B, world, rank)      # weak scaling: B instances per GPU
     assert count == B
     x0_host = synthetic_x0(B, offset, ctx)
-    pub = Publisher(B, dev, world) if world > 1 and not args.no_allgather else None
+    pub = Publisher(B, dev, world) if distributed and not args.no_allgather else None
     loop = FleetLoop(GpuStepper(ctx), torch.from_numpy(x0_host).to(dev), N, cfg.dt, ekf=args.ekf,
                      covariances=ok.ekf_default_covariances() if args.ekf else None, publisher=pub)
 
     for _ in range(args.warmup):
         loop.step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ctx.timing_start(args.steps)
@@ -316,7 +320,7 @@ def main():
     for _ in range(args.steps):
         loop.step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -376,7 +380,8 @@ def main():
             "config": {"workload": workload, "ekf": bool(args.ekf),
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
-                       "allgather": bool(world > 1 and not args.no_allgather)},
+                       "allgather": pub is not None,
+                       "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items()},
@@ -396,7 +401,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

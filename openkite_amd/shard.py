@@ -42,7 +42,7 @@ class Publisher:
     def publish(self, u0: torch.Tensor, diag: torch.Tensor) -> torch.Tensor:
         self.pub[:, :4].copy_(u0)
         self.pub[:, 4:].copy_(diag)
-        if self.world == 1:
+        if not dist.is_initialized():
             self.gathered.copy_(self.pub)
         elif self._nccl:
             dist.all_gather_into_tensor(self.gathered, self.pub)
@@ -54,6 +54,6 @@ class Publisher:
 def max_over_ranks(seconds: float, device) -> float:
     """Wall time of the slowest rank (the job's time)."""
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
