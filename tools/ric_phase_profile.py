@@ -43,6 +43,6 @@ for i, p in enumerate(PHASES):
     print(f"{p:22s} {c:12.0f} cycles/kite  {100 * c / tot:5.1f}%  per-iteration {per_it:10.0f}")
 print(f"{'total':22s} {tot:12.0f}")
 sv = np.array(sub[:8], dtype=np.float64) / nk / (its / nk) / NH
-for i, nm in enumerate(["Z wait + p vector", "adjoint", "T, M MFMAs", "readlane/bcast/border", "chol4 + S", "transpose + rank-4", "s^ + p"]):
+for i, nm in enumerate(["Z wait", "tail(k+1) + head(k)", "T, M MFMAs", "readlane/bcast/border", "chol4 + S", "transpose + rank-4", "carry"]):
     print(f"  factor stage: {nm:24s} {sv[i]:8.0f} cycles per stage")
 g.close()
