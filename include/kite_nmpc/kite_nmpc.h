@@ -272,6 +272,9 @@ typedef struct kite_colloc_config {
     double mayer_scale;     /* 1 (NMPF), 2 (full_generics_test)                   */
     double Sx[15], Su[4];   /* 1 = unscaled                                       */
     double path_radius, path_altitude, path_q[4];
+    int32_t path_harmonics;  /* as kite_nmpc_config (API 3): 0 the circle, 1..8 Fourier path */
+    int32_t reserved2;
+    double path_fourier[3][2 * KITE_PATH_MAX_HARMONICS + 1];
 } kite_colloc_config;
 /* The NMPF's setup (kiteNMPF.cpp:80-143 with the node's scaling and path).  */
 void kite_colloc_default_config(kite_colloc_config* cfg);

@@ -744,6 +744,8 @@ void kite_colloc_default_config(kite_colloc_config* c) {
     c->mayer_scale = 1.0;
     c->path_radius = n.path_radius; c->path_altitude = n.path_altitude;
     for (int i = 0; i < 4; ++i) c->path_q[i] = n.path_q[i];
+    c->path_harmonics = n.path_harmonics;
+    std::memcpy(c->path_fourier, n.path_fourier, sizeof(c->path_fourier));
 }
 
 int kite_nmpc_colloc_eval(kite_nmpc_ctx* ctx, const kite_colloc_config* cfg, int32_t count, const double* z,
@@ -779,6 +781,10 @@ int kite_nmpc_colloc_eval(kite_nmpc_ctx* ctx, const kite_colloc_config* cfg, int
     C.W = cfg->W; C.vref = cfg->vref;
     C.path_R = cfg->path_radius; C.path_alt = cfg->path_altitude;
     for (int i = 0; i < 4; ++i) C.pq[i] = cfg->path_q[i];
+    if (cfg->path_harmonics < 0 || cfg->path_harmonics > KITE_PATH_MAX_HARMONICS) return KITE_EINVAL;
+    C.path_K = cfg->path_harmonics;
+    for (int a = 0; a < 3; ++a)
+        for (int j = 0; j < KITE_PATH_NC; ++j) C.pF[a][j] = cfg->path_harmonics ? cfg->path_fourier[a][j] : 0.0;
 
     const size_t c = count, nz = (size_t)n * 19, ng = (size_t)n * 15, nj = jac ? c * n * 15 * 19 : 0;
     int rc = ensure_scratch(ctx, (tab.size() + c * nz + c * ng + c + nj) * sizeof(double));

@@ -97,6 +97,8 @@ class CollocConfig(ctypes.Structure):
         ("W", ctypes.c_double), ("vref", ctypes.c_double), ("mayer_scale", ctypes.c_double),
         ("Sx", ctypes.c_double * 15), ("Su", ctypes.c_double * 4),
         ("path_radius", ctypes.c_double), ("path_altitude", ctypes.c_double), ("path_q", ctypes.c_double * 4),
+        ("path_harmonics", ctypes.c_int32), ("reserved2", ctypes.c_int32),
+        ("path_fourier", ctypes.c_double * (3 * PATH_NC)),
     ]
 
     def to_dict(self) -> dict:

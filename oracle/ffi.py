@@ -167,8 +167,12 @@ def colloc_vector(c: Dict) -> np.ndarray:
     for k in COLLOC_KEYS:
         x = c[k]
         v.extend(x if isinstance(x, (list, tuple, np.ndarray)) else [x])
-    a = np.array(v, dtype=np.float64)
-    assert a.size == 40
+    F = np.zeros((3, 17))
+    K = int(c.get("path_harmonics", 0))
+    if K:
+        F[:] = np.asarray(c["path_fourier"], dtype=np.float64).reshape(3, 17)
+    a = np.concatenate([np.array(v, dtype=np.float64), [float(K)], F.reshape(-1)])
+    assert a.size == 92
     return a
 
 

@@ -44,18 +44,20 @@ def test_struct_layouts_match_header():
     assert ok.lib().kite_nmpc_api_version() == 3
 
 
-def test_config_layout_matches_c_compiler(tmp_path):
-    """sizeof / offsetof of kite_nmpc_config from a C compiler == the ctypes mirror."""
+@pytest.mark.parametrize("cname,py", [("kite_nmpc_config", "NmpcConfig"), ("kite_colloc_config", "CollocConfig")])
+def test_config_layout_matches_c_compiler(tmp_path, cname, py):
+    """sizeof / offsetof of the config structs from a C compiler == the ctypes mirrors."""
+    S = getattr(ok.nmpc, py)
     src = tmp_path / "lay.c"
-    fields = [f for f, _ in ok.NmpcConfig._fields_]
+    fields = [f for f, _ in S._fields_]
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "kite_nmpc/kite_nmpc.h"\nint main(void){'
-                   + 'printf("%zu\\n", sizeof(kite_nmpc_config));'
-                   + "".join(f'printf("%zu\\n", offsetof(kite_nmpc_config, {f}));' for f in fields) + "return 0;}")
+                   + f'printf("%zu\\n", sizeof({cname}));'
+                   + "".join(f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields) + "return 0;}")
     exe = tmp_path / "lay"
     subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ok.nmpc.REPO, "include"), "-o", str(exe), str(src)], check=True)
     out = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    assert out[0] == ctypes.sizeof(ok.NmpcConfig)
-    assert out[1:] == [getattr(ok.NmpcConfig, f).offset for f in fields]
+    assert out[0] == ctypes.sizeof(S)
+    assert out[1:] == [getattr(S, f).offset for f in fields]
 
 
 def test_load_properties_matches_yaml_and_oracle():

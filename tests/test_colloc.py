@@ -89,17 +89,48 @@ def test_oracle_residual_of_a_linear_trajectory(kp):
     np.testing.assert_allclose(G + ts * sode, np.tile(slope, (n, 1)), rtol=1e-11, atol=1e-11)
 
 
+def fourier_colloc_cfg():
+    """The NMPF setup on the three-harmonic path of tests/test_path.py."""
+    from test_path import fourier_path
+    F = np.zeros((3, 17)); F[:, :7] = fourier_path()
+    cfg = ok.colloc_default_config()
+    cfg.path_harmonics = 3
+    for i, v in enumerate(F.reshape(-1)):
+        cfg.path_fourier[i] = v
+    return cfg
+
+
+def test_oracle_colloc_circle_as_fourier(kp):
+    """The collocation cost on the node's circle written as a K = 1 Fourier
+    curve equals the circle's (oracle); a non-circular path changes it."""
+    c0 = nmpf_cfg()
+    c1 = dict(c0, path_harmonics=1)
+    F = np.zeros((3, 17)); F[0, 1] = c0["path_radius"]; F[1, 2] = c0["path_radius"]; F[2, 0] = c0["path_altitude"]
+    c1["path_fourier"] = F.reshape(-1)
+    z = nmpf_points(16)
+    G0, J0 = ffi.colloc_eval(kp, c0, z)
+    G1, J1 = ffi.colloc_eval(kp, c1, z)
+    np.testing.assert_array_equal(G0, G1)
+    np.testing.assert_allclose(J0, J1, rtol=1e-14)
+    _, J2 = ffi.colloc_eval(kp, fourier_colloc_cfg().to_dict(), z)
+    assert np.abs(J2 - J0).max() > 1e-3 * np.abs(J0).max()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("which", ["full_generics", "nmpf"])
+@pytest.mark.parametrize("which", ["full_generics", "nmpf", "nmpf_fourier"])
 def test_gpu_colloc_vs_oracle(kp, which):
     if which == "full_generics":
         c = FIX["config"]
         z = np.array(FIX["z"])[None]
         cfg = ok.colloc_default_config(**{k: v for k, v in c.items() if k != "lines"})
-    else:
+    elif which == "nmpf":
         c = nmpf_cfg()
         z = nmpf_points(512)
         cfg = ok.colloc_default_config()
+    else:
+        cfg = fourier_colloc_cfg()
+        c = cfg.to_dict()
+        z = nmpf_points(512)
     g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), 1)
     try:
         G, J, Jb = g.colloc_eval(cfg, z, jac=True)
