@@ -203,7 +203,7 @@ int validate_config(const kite_nmpc_config& c) {
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
     if (c.qp_kernel < 0 || c.qp_kernel > 3) return KITE_EINVAL;
-    if (!(c.qp_soft_weight > 2.0 * 20.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;   // > 2 z0 (RIC_Z0)
+    if (!(c.qp_soft_weight > 2.0 * 10.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;   // > 2 z0 (RIC_Z0)
     if (!(c.qp_lm >= 0.0) || !std::isfinite(c.qp_lm)) return KITE_EINVAL;
     if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
     if (!(c.delay >= 0.0) || !std::isfinite(c.delay) || std::lround(c.delay / c.dt) > c.N) return KITE_EINVAL;
