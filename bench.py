@@ -84,6 +84,32 @@ def synthetic_x0(B, offset, ctx):
     return x
 
 
+def gpu_single_kite_latency(args, ok, x1, steps=200, warm=20):
+    """One kite per context, the ROS node's use (nmpf_node.cpp:206-246 calls
+    computeControl for its one kite): wall time of the host entry point
+    kite_nmpc_step (state in, control + plan out, PCIe both ways, stream
+    synchronised) over a warm closed loop.  Not `value` (which is batch
+    throughput with inputs in HBM); reported beside the CPU oracle's
+    single-thread batch-1 latency."""
+    cfg = ok.default_config(N=args.horizon, M=args.substeps, qp_iters=args.qp_iters)
+    cfg.qp_kernel = args.qp_kernel
+    cfg.sens_fp32 = 1 if args.fp32_sens else 0
+    g = ok.BatchNMPC(ok.load_properties(), cfg, 1)
+    try:
+        x = x1.copy()
+        ts = []
+        for i in range(warm + steps):
+            t0 = time.perf_counter()
+            r = g.step(x)
+            ts.append(time.perf_counter() - t0)
+            x = r["traj"][:, 1, :].copy()
+        t = np.array(ts[warm:]) * 1e3
+    finally:
+        g.close()
+    return {"median_ms": round(float(np.median(t)), 4), "p90_ms": round(float(np.percentile(t, 90)), 4),
+            "steps": steps, "api": "kite_nmpc_step (host arrays, synchronous)"}
+
+
 def host_cpu_info():
     """What the CPU numbers ran on: the machine's CPUs, this process's CPU set
     and cgroup quota, and the thread count the box allots (OMP_NUM_THREADS)."""
@@ -360,6 +386,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, x0_host, args.cpu_seconds)
+        # beside the CPU baseline only (the profiled runs pass --no-cpu-baseline and
+        # must see the batch launches alone)
+        lat1 = gpu_single_kite_latency(args, ok, x0_host[:1]) if world == 1 and not args.no_cpu_baseline else None
         workload = (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
                     + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
                     + (" + fused EKF (BASELINE configs[4])" if args.ekf else
@@ -384,6 +413,7 @@ def main():
                        "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "gpu_latency_batch1": lat1,
             "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items()},
             "interval_integrations_per_s": round(world * B * N / (avg_ms["rk4_sens"] * 1e-3), 1)
             if avg_ms["rk4_sens"] > 0 else None,
