@@ -176,3 +176,39 @@ def test_gpu_rti_fourier_path_vs_oracle(kp, Nh):
             x = Xo[:, 1, :].copy()
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Nh", [20, 40])
+def test_gpu_single_kite_fourier_path_with_delay_vs_oracle(kp, Nh):
+    """The ROS node's use on an arbitrary path: ONE kite per context (B = 1),
+    the fused transport-delay compensation (0.1 s, nmpf_node.cpp:74, 16 RK4
+    substeps) and the three-harmonic path, 8 closed-loop steps against the
+    oracle with a plant that drifts from the prediction."""
+    from test_gpu_parity import RTI_TOL, assert_ms_rti, rel_per_kite
+    B, M, K = 1, 2, 16
+    F = fourier_path()
+    oc = oracle_config(F, N=Nh)
+    oc["delay"], oc["delay_steps"] = 0.1, 16
+    if Nh == 20:
+        oc["qp_form"] = 0
+    cv = ffi.cfg_vector(oc)
+    x = x0_on_path(cv, B, offset=5100)
+    g = ok.BatchNMPC(ok.load_properties(), product_config(F, N=Nh, delay=0.1, delay_steps=16), B)
+    Xo = np.zeros((B, Nh + 1, 15)); Uo = np.zeros((B, Nh, 4))
+    try:
+        for step in range(8):
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
+            if Nh == 20:
+                e = max(rel(r["u0"], u0), rel(r["traj"], Xo), rel(r["ctrl"], Uo))
+                assert e < RTI_TOL, (step, e)
+            else:
+                e = np.maximum(rel_per_kite(r["traj"], Xo), rel_per_kite(r["ctrl"], Uo))
+                assert_ms_rti(e, g.qp_stats()[0], diag[:, 5], (Nh, step))
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2)
+            x = Xo[:, 1, :].copy()
+            x[:, :3] *= 1.002
+            x[:, 13:] = 0.0
+    finally:
+        g.close()
