@@ -353,6 +353,7 @@ def main():
     nrec, ksum = ctx.timing_read()
     kkt, iters = ctx.qp_stats()
     it_sum = ctx.qp_iteration_sum()
+    b_steps, b_rows = ctx.state_bound_stats()
     status = loop.status.cpu().numpy()
 
     elapsed_max = max_over_ranks(elapsed, dev)
@@ -421,6 +422,13 @@ def main():
             "qp_mean_iterations": round(mean_it, 3),
             "qp_converged_frac": round(float(np.mean(kkt < 1e-8)), 5),
             "status_nan": int(np.sum(status & 1)),
+            "state_bounds": {"kite_steps_outside": b_steps, "rows_outside": b_rows,
+                             "kite_steps": B * args.steps,
+                             "note": "over the timed steps: committed plans leaving the state box |omega_i| <= 4 pi, "
+                                     "|q_i| <= 1.01 (nmpf_node.cpp:59-63; status bit 8) and their (node, state) pairs "
+                                     "outside it" + ("; multiple-shooting QP: soft rows with xi > 0 at the accepted "
+                                                     "solution" if ok.resolve_qp_kernel(args.qp_kernel, N) == 3
+                                                     else "; condensed QP: after the lazy rows (DESIGN 4.4)")},
             "status_last_step": {name: int(np.sum((status & bit) != 0)) for name, bit in
                                  (("nan", 1), ("qp_not_converged", 2), ("state_bound", 8), ("rejected", 32),
                                   ("restart", 64))},

@@ -35,10 +35,11 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 3   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+#define KITE_NMPC_API_VERSION 4   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
                                       qp_kernel 3 (multiple-shooting QP, Riccati IPM);
                                    3: kite_nmpc_config gained path_harmonics, path_fourier
-                                      (arbitrary closed paths); delay_steps default 16 */
+                                      (arbitrary closed paths); delay_steps default 16;
+                                   4: kite_nmpc_state_bound_stats (no config change) */
 #define KITE_PATH_MAX_HARMONICS 8 /* Fourier path: harmonics per axis              */
 
 /* ---- error codes ------------------------------------------------------ */
@@ -312,6 +313,14 @@ int kite_nmpc_qp_stats(kite_nmpc_ctx* ctx, double* kkt, int32_t* iters);
  * the last kite_nmpc_timing_start (or since create): the measurement hook
  * behind bench.py's FLOP count (no reference counterpart).                */
 int kite_nmpc_qp_iteration_sum(kite_nmpc_ctx* ctx, int64_t* sum);
+/* State-box enforcement since the last kite_nmpc_timing_start (or since
+ * create), summed over instances and steps: kite-steps whose committed plan
+ * leaves the state box (status bit 8) and the (node, state) pairs outside it
+ * (states 1..12, nodes 1..N, tolerance 1e-8 max(1, |bound|)); with the
+ * multiple-shooting QP the latter are the soft rows with xi > 0 at the
+ * accepted solution.  The reference's NLP holds these as hard bounds
+ * (kiteNMPF.cpp:154-167); measurement hook, either pointer may be NULL.    */
+int kite_nmpc_state_bound_stats(kite_nmpc_ctx* ctx, int64_t* steps_outside, int64_t* rows_outside);
 /* Condensed QP of one instance from the last step (scaled variables, GPU
  * column order: [T,dE,dR]_k (3N) | Uv_k (N) | theta0 | thetadot0).
  * H n x n, h n, C N x n, cl/cu N (+-INF = absent), n = 4N+2.               */

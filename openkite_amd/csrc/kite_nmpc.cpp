@@ -479,11 +479,14 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         (void)hipMemset(*a.p, 0, a.count * sizeof(double));
     }
     if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&ctx->iters, 2 * B * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&ctx->iters, 4 * B * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->order, (2 * (size_t)B + 1) * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->dconst, 4096) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
     (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
-    (void)hipMemset(ctx->iters, 0, 2 * B * sizeof(int32_t));   // [0, B): last step, [B, 2B): running sum
+    // [0, B): QP iterations of the last step; running sums since timing_start:
+    // [B, 2B) QP iterations, [2B, 3B) steps ending outside the state box (status
+    // bit 8), [3B, 4B) (node, state) pairs outside it (kite_nmpc_state_bound_stats)
+    (void)hipMemset(ctx->iters, 0, 4 * B * sizeof(int32_t));
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
         free_ctx(ctx); delete ctx; return KITE_EHIP;
     }
@@ -927,8 +930,8 @@ int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
     }
     ctx->ring_cap = max_steps;
     ctx->ring_used = 0;
-    // restart the per-instance QP iteration sums (second half of ctx->iters)
-    HIP_TRY(hipMemsetAsync(ctx->iters + ctx->B, 0, (size_t)ctx->B * sizeof(int32_t), ctx->stream));
+    // restart the per-instance running sums (ctx->iters[B, 4B))
+    HIP_TRY(hipMemsetAsync(ctx->iters + ctx->B, 0, 3 * (size_t)ctx->B * sizeof(int32_t), ctx->stream));
     return KITE_OK;
 }
 
@@ -975,6 +978,20 @@ int kite_nmpc_qp_iteration_sum(kite_nmpc_ctx* ctx, int64_t* sum) {
     int64_t t = 0;
     for (int32_t v : acc) t += v;
     *sum = t;
+    return KITE_OK;
+}
+
+int kite_nmpc_state_bound_stats(kite_nmpc_ctx* ctx, int64_t* steps_outside, int64_t* rows_outside) {
+    if (!ctx) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<int32_t> acc(2 * (size_t)ctx->B);
+    HIP_TRY(hipMemcpyAsync(acc.data(), ctx->iters + 2 * ctx->B, acc.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int64_t a = 0, r = 0;
+    for (int i = 0; i < ctx->B; ++i) { a += acc[i]; r += acc[(size_t)ctx->B + i]; }
+    if (steps_outside) *steps_outside = a;
+    if (rows_outside) *rows_outside = r;
     return KITE_OK;
 }
 

@@ -1163,7 +1163,8 @@ __device__ __forceinline__ void rti_commit(const RtiConst& C, int b, int l, doub
                                            double* __restrict__ Xb, double* __restrict__ Ub,
                                            double* __restrict__ u0_out, double* __restrict__ diag,
                                            int32_t* __restrict__ status, double* __restrict__ kkt_out,
-                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ iters_acc) {
+                                           int32_t* __restrict__ iters_out, int32_t* __restrict__ iters_acc,
+                                           int B) {
     const int N = C.N;
     const bool accept = kkt < QP_STEP_ACCEPT;
     for (int k = l; k <= N; k += 64) {
@@ -1181,7 +1182,7 @@ __device__ __forceinline__ void rti_commit(const RtiConst& C, int b, int l, doub
     if constexpr (WAVE) wave_sync(); else __syncthreads();
 
     // ---- diagnostics, cost, status -------------------------------------------
-    double cost = 0.0;
+    double cost = 0.0, nrow = 0.0;
     int bad = 0, bound = 0;
     for (int k = l; k <= N; k += 64) {
         const double* xk = Xb + k * NX;
@@ -1206,10 +1207,11 @@ __device__ __forceinline__ void rti_commit(const RtiConst& C, int b, int l, doub
         if (k >= 1)
             for (int i = 1; i < 13; ++i) {
                 const double lb = sbnd[i], ub = sbnd[16 + i];
-                if (xk[i] < lb - bound_tol(lb) || xk[i] > ub + bound_tol(ub)) bound = 1;
+                if (xk[i] < lb - bound_tol(lb) || xk[i] > ub + bound_tol(ub)) { bound = 1; nrow += 1.0; }
             }
     }
     cost = wave_sum(cost);
+    nrow = wave_sum(nrow);
     bad = wave_or(bad);
     bound = wave_or(bound);
     if (l == 0) {
@@ -1232,7 +1234,11 @@ __device__ __forceinline__ void rti_commit(const RtiConst& C, int b, int l, doub
         status[b] = st;
         if (kkt_out) kkt_out[b] = kkt;
         if (iters_out) iters_out[b] = iters;
-        if (iters_acc) iters_acc[b] += iters;          // running sum since kite_nmpc_timing_start
+        if (iters_acc) {                               // running sums since kite_nmpc_timing_start
+            iters_acc[b] += iters;
+            iters_acc[B + b] += (bound && !bad) ? 1 : 0;        // kite-steps ending outside the state box
+            iters_acc[2 * B + b] += bad ? 0 : (int32_t)nrow;    // (node, state) pairs outside it
+        }
         for (int c = 0; c < NU; ++c) u0_out[(size_t)b * NU + c] = Ub[c];
     }
 }
@@ -1748,7 +1754,7 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
     init_rows();
     }
     rti_commit(C, b, l, kkt, iters, vec, dxs, sbnd, Xb, Ub, u0_out, diag, status, kkt_out, iters_out,
-               iters_out ? iters_out + B : nullptr);
+               iters_out ? iters_out + B : nullptr, B);
 }
 
 // the fast instance over the whole grid (LPT order); the lazy instance over

@@ -156,6 +156,8 @@ _SIGNATURES = {
     "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
     "kite_nmpc_qp_iteration_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "kite_nmpc_state_bound_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                                   ctypes.POINTER(ctypes.c_int64)]),
     "kite_ekf_default_covariances": (None, [_DP, _DP, _DP]),
     "kite_colloc_default_config": (None, [ctypes.c_void_p]),
     "kite_nmpc_colloc_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP]),
@@ -349,6 +351,14 @@ class BatchNMPC:
         v = ctypes.c_int64(0)
         _check(lib().kite_nmpc_qp_iteration_sum(self._h, ctypes.byref(v)), "qp_iteration_sum")
         return int(v.value)
+
+    def state_bound_stats(self):
+        """(kite-steps outside the state box, (node, state) pairs outside it),
+        summed over instances and steps since timing_start (status bit 8 and
+        the violated state rows of the committed plans)."""
+        a, r = ctypes.c_int64(0), ctypes.c_int64(0)
+        _check(lib().kite_nmpc_state_bound_stats(self._h, ctypes.byref(a), ctypes.byref(r)), "state_bound_stats")
+        return int(a.value), int(r.value)
 
     def get_qp(self, instance: int):
         n = 4 * self.N + 2

@@ -118,6 +118,9 @@ def lib():
             "orc_qp_solve": (d, [i, i, dp, dp, dp, dp, dp, dp, i, dp]),
             "orc_prologue": (i, [dp, dp, i, i, dp, i, i, dp, dp, dp]),
             "orc_msqp_solve": (d, [dp, dp, i, i, dp, dp, i, dp, ip]),
+            "orc_msqp_solve_pert": (d, [dp, dp, i, i, dp, dp, i, d, i, dp, ip]),
+            "orc_set_ms_z0": (None, [d]),
+            "orc_get_ms_z0": (d, []),
             "orc_msqp_build": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
             "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i, ip]),
             "orc_traj_cost": (d, [dp, i, dp, dp]),
@@ -271,6 +274,27 @@ def msqp_solve(kp, cfgv, N, M, X, U, K):
     kkt = lib().orc_msqp_solve(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), int(K), _p(v),
                                it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
     return v, kkt, int(it[0])
+
+
+def msqp_solve_perturbed(kp, cfgv, N, M, X, U, K, eps, seed):
+    """msqp_solve with the QP data (A, B, d, J, r, Rh, rho) perturbed by a
+    relative eps * N(0, 1) per element (fixed seed): the QP's sensitivity
+    envelope under rounding-level differences."""
+    nv = (N + 1) * 15 + N * 4
+    v = np.zeros(nv)
+    it = np.zeros(1, dtype=np.int32)
+    kkt = lib().orc_msqp_solve_pert(_p(kp), _p(cfgv), N, M, _p(_f64(X)), _p(_f64(U)), int(K), float(eps),
+                                    int(seed), _p(v), it.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return v, kkt, int(it[0])
+
+
+def set_ms_z0(z0: float) -> float:
+    """Start multiplier of the oracle's multiple-shooting IPM (tools only; the
+    GPU kernel has its own constant RIC_Z0).  Returns the previous value."""
+    L = lib()
+    old = L.orc_get_ms_z0()
+    L.orc_set_ms_z0(float(z0))
+    return old
 
 
 def msqp_build(kp, cfgv, N, M, X, U):

@@ -49,10 +49,20 @@ COND40_ENVELOPE = 1e-4  # condensed QP at N = 40 (qp_kernel 1 / 2, the before-pi
                         # a 1e-15 relative perturbation of H
 
 
+MS_ENVELOPE = 3e-5  # multiple-shooting QP frozen on both sides: a 1e-15 relative perturbation
+                    # of the QP data moves the oracle's own frozen solution by up to 1.2e-5 when
+                    # the IPM then freezes one iteration earlier or later (5e-9 otherwise;
+                    # tests/test_oracle.py::test_ms_qp_sensitivity_envelope)
+
+
 def assert_ms_rti(e, kkt_gpu, kkt_orc, where):
-    """RTI bar on every QP frozen on both sides, MS_CAP_TOL on the rest."""
+    """Multiple-shooting QP: every QP frozen on both sides within its measured
+    sensitivity envelope MS_ENVELOPE and >= 99.5 % of them within RTI_TOL;
+    MS_CAP_TOL on the rest."""
     frozen = (kkt_gpu < 1e-10) & (kkt_orc < 1e-10)
-    assert e[frozen].max(initial=0.0) < RTI_TOL, (where, np.sort(e[frozen])[-5:])
+    ef = e[frozen]
+    assert ef.max(initial=0.0) < MS_ENVELOPE, (where, np.sort(ef)[-5:])
+    assert np.mean(ef < RTI_TOL) >= 0.995 if ef.size else True, (where, np.sort(ef)[-5:])
     assert e[~frozen].max(initial=0.0) < MS_CAP_TOL, (where, np.sort(e[~frozen])[-5:])
     return int(frozen.sum())
 
@@ -280,6 +290,7 @@ def test_long_closed_loop_vs_oracle(kp, cfgv):
     rejected = 0
     errs = []
     try:
+        g.timing_start(steps)
         for step in range(steps):
             if step > 0:
                 g.set_solution(Xo, Uo)
@@ -545,6 +556,7 @@ def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_fra
     diverged = np.zeros(B, bool)
     errs = []
     try:
+        g.timing_start(steps)
         for step in range(steps):
             if step > 0:
                 g.set_solution(Xo, Uo)
@@ -560,6 +572,9 @@ def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_fra
             errs.append(e)
             assert np.mean(e < tol) >= err_frac and e.max() < max_err, (label, step, np.sort(e)[-5:])
             x = Xo[:, 1, :].copy()
+        # state-box accounting over the loop (kite_nmpc_state_bound_stats): no
+        # committed plan leaves the box, as the per-step bit-8 checks above say
+        assert g.state_bound_stats() == (0, 0), g.state_bound_stats()
     finally:
         g.close()
     assert diverged.sum() <= (max_diverged if max_diverged is not None else B // 1000), np.where(diverged)[0]
@@ -585,33 +600,37 @@ def test_config4_fp32_sensitivities_full_batch_vs_fp64_oracle(kp, cfgv):
                                max_err=1e-2)
 
 
-def test_config5_n40_fused_ekf_vs_oracle(kp):
-    """BASELINE config 5: N = 40 with the fused EKF -> RTI sequence bench.py
-    times (openkite_amd/fleet.py: 5 EKF propagation substeps of dt/5 under the
-    applied control, update with the measured position + attitude, RTI from
-    the estimate), 256 kites x 12 closed-loop steps on torch's stream -- past
-    steps 5-9, where the condensed formulation's NaN / restart storms began
-    (profiles/r02z_oracle_n40_closed_loop_status.txt).  Every step, the oracle
-    repeats the sequence from the GPU loop's own state before the step
-    (estimate, covariance, measurement, applied control, warm start), so each
-    step is a parity check from identical inputs.  Per kite and step: status
-    words equal (NaN, restart, rejected, bound, min-speed, wrap; the not-
-    converged bit may differ only where the two residuals straddle its 1e-8
-    threshold), the RTI bar on every QP frozen on both sides, MS_CAP_TOL on
-    the rest; no NaN, no rejected step, no restart anywhere."""
+def _rows_outside(kp_cfg, X):
+    """(node, state) pairs of plans X (B, N+1, 15) outside the state box
+    (states 1..12, nodes 1..N, tolerance 1e-8 max(1, |bound|)), per kite."""
+    lb, ub = np.asarray(kp_cfg["lbx"], float), np.asarray(kp_cfg["ubx"], float)
+    tl = 1e-8 * np.maximum(1.0, np.abs(lb)); tu = 1e-8 * np.maximum(1.0, np.abs(ub))
+    x = X[:, 1:, 1:13]
+    out = (x < (lb - tl)[1:13]) | (x > (ub + tu)[1:13])
+    return out.reshape(X.shape[0], -1).sum(1)
+
+
+def _config5_vs_oracle(kp, B, steps, offset):
+    """BASELINE config 5's sequence (N = 40 + fused EKF, bench.py's loop) on the
+    GPU against the oracle from identical inputs every step (see the test
+    docstrings); also the state-box accounting of kite_nmpc_state_bound_stats
+    against the oracle's plans."""
     torch = pytest.importorskip("torch")
     from openkite_amd.fleet import FleetLoop, GpuStepper
-    B, Nh, steps = 256, 40, 12
-    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    Nh = 40
+    node = ffi.node_config(N=Nh)
+    cv = ffi.cfg_vector(node)
     cfg = ok.default_config(N=Nh)
     assert ok.resolve_qp_kernel(cfg.qp_kernel, Nh) == 3
     g = ok.BatchNMPC(ok.load_properties(), cfg, B)
     W, V, P0 = ok.ekf_default_covariances()
-    frozen_total = 0
+    frozen_total, errs = 0, []
+    orc_bound_steps = orc_rows = 0
     try:
         g.set_stream(torch.cuda.current_stream().cuda_stream)
-        x0 = x0_batch(B, offset=11000)
+        x0 = x0_batch(B, offset=offset)
         loop = FleetLoop(GpuStepper(g), torch.from_numpy(x0).cuda(), Nh, cfg.dt, ekf=True, covariances=(W, V, P0))
+        g.timing_start(steps)
         for step in range(steps):
             torch.cuda.synchronize()
             xe, P = loop.xe.cpu().numpy(), loop.P.cpu().numpy()
@@ -634,12 +653,49 @@ def test_config5_n40_fused_ekf_vs_oracle(kp):
             assert np.all(((stg & 2) == (st & 2)) | straddle), step
             assert not np.any(stg & (1 | 32 | 64)), (step, np.unique(stg))
             e = rel_per_kite(tr, Xo)
+            errs.append(e)
             frozen_total += assert_ms_rti(e, kg, ko, step)
+            orc_bound_steps += int(np.sum((st & 8) != 0))
+            orc_rows += int(_rows_outside(node, Xo).sum())
         assert np.all(np.isfinite(loop.traj.cpu().numpy()))
         assert frozen_total >= 0.9 * B * steps, frozen_total
+        b_steps, b_rows = g.state_bound_stats()
     finally:
         g.close()
-    print(f"config 5: {B} kites x {steps} steps, {frozen_total} QPs frozen on both sides")
+    # state-box enforcement (ADVICE / VERDICT r03): the GPU's accounting equals
+    # the oracle's plans kite-step by kite-step in sum (status bit 8 is already
+    # compared per kite above), and the soft rows end inside the box
+    assert b_steps == orc_bound_steps and b_rows == orc_rows, (b_steps, orc_bound_steps, b_rows, orc_rows)
+    e = np.concatenate(errs)
+    print(f"config 5: {B} kites x {steps} steps, {frozen_total} QPs frozen on both sides; errors median "
+          f"{np.median(e):.1e} p99.9 {np.quantile(e, 0.999):.1e} max {e.max():.1e}; state box: {b_steps} kite-steps, "
+          f"{b_rows} soft rows outside")
+    return b_steps, b_rows
+
+
+def test_config5_n40_fused_ekf_vs_oracle(kp):
+    """BASELINE config 5: N = 40 with the fused EKF -> RTI sequence bench.py
+    times (openkite_amd/fleet.py: 5 EKF propagation substeps of dt/5 under the
+    applied control, update with the measured position + attitude, RTI from
+    the estimate), 256 kites x 12 closed-loop steps on torch's stream -- past
+    steps 5-9, where the condensed formulation's NaN / restart storms began
+    (profiles/r02z_oracle_n40_closed_loop_status.txt).  Every step, the oracle
+    repeats the sequence from the GPU loop's own state before the step
+    (estimate, covariance, measurement, applied control, warm start), so each
+    step is a parity check from identical inputs.  Per kite and step: status
+    words equal (NaN, restart, rejected, bound, min-speed, wrap; the not-
+    converged bit may differ only where the two residuals straddle its 1e-8
+    threshold), assert_ms_rti's envelope bars on every QP frozen on both sides,
+    MS_CAP_TOL on the rest; no NaN, no rejected step, no restart anywhere."""
+    _config5_vs_oracle(kp, 256, 12, 11000)
+
+
+def test_config5_full_batch_vs_oracle(kp):
+    """BASELINE config 5 at its own size: 4096 kites, N = 40 + fused EKF, 3
+    closed-loop steps, the same per-kite bars as the 256-kite test; the
+    state-box accounting of the step (kite_nmpc_state_bound_stats: kite-steps
+    and soft rows outside the box) equals the oracle's."""
+    _config5_vs_oracle(kp, 4096, 3, 12000)
 
 
 @pytest.mark.parametrize("fp32", [0, 1])

@@ -254,3 +254,42 @@ def test_prologue_restarts_on_nonfinite_plan(kp, cfgv):
     np.testing.assert_array_equal(Xw, Xc)
     np.testing.assert_array_equal(Uw, Uc)
     assert st2 & 64 == 0
+
+
+MS_ENVELOPE = 3e-5   # the multiple-shooting QP's frozen-solution envelope (see below); the
+                     # bar of tests/test_gpu_parity.py::assert_ms_rti for QPs frozen on both sides
+
+
+def test_ms_qp_sensitivity_envelope(kp):
+    """Intrinsic sensitivity of the multiple-shooting QP (qp_form 1, N = 40:
+    BASELINE config 5) on closed-loop inputs: the QP data (A_k, B_k, d_k, J_k,
+    r_k, R, rho) perturbed by a relative 1e-15 -- rounding-level differences
+    between two fp64 implementations -- and solved again.  Where the perturbed
+    IPM takes the same number of iterations the frozen solutions agree to
+    ~1e-9; where it freezes one iteration earlier or later they move by up to
+    ~1e-5 (tools/ms_envelope_probe.py 512 23 40: 5 of 23 512 perturbed solves,
+    max 1.2e-5; same count: max 5.3e-9).  That sets assert_ms_rti's bar:
+    MS_ENVELOPE for every QP frozen on both sides, RTI_TOL for >= 99.5 % of them."""
+    from tests.test_gpu_parity import x0_batch
+    Nh, M, K, B, steps = 40, 2, 16, 96, 8
+    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    x = x0_batch(B, offset=11000)
+    X = np.zeros((B, Nh + 1, 15)); U = np.zeros((B, Nh, 4))
+    same, moved = [], []
+    for step in range(steps):
+        for b in range(B):
+            st, Xp, Up, _ = ffi.prologue(kp, cv, Nh, M, x[b], X[b], U[b], warm=int(step > 0))
+            v0, k0, i0 = ffi.msqp_solve(kp, cv, Nh, M, Xp, Up, K)
+            v1, k1, i1 = ffi.msqp_solve_perturbed(kp, cv, Nh, M, Xp, Up, K, 1e-15, 1000 * b + step)
+            if k0 < 1e-10 and k1 < 1e-10:
+                e = np.abs(v1 - v0).max() / max(1.0, np.abs(v0).max())
+                (same if i0 == i1 else moved).append(e)
+        ffi.rti_step(kp, cv, Nh, M, K, x, X, U, warm=int(step > 0), nthreads=0)
+        x = X[:, 1, :].copy()
+    same, moved = np.array(same), np.array(moved)
+    assert same.size + moved.size >= 0.99 * B * steps
+    assert same.max() < 1e-7, same.max()
+    assert moved.max(initial=0.0) < MS_ENVELOPE, moved
+    assert np.mean(np.concatenate([same, moved]) < 1e-6) >= 0.995
+    print(f"MS QP envelope: {same.size} same-count solves max {same.max():.1e}, "
+          f"{moved.size} with a changed count max {moved.max(initial=0.0):.1e}")
