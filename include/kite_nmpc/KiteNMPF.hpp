@@ -91,7 +91,8 @@ public:
         setPath(path);
     }
     // the reference declares setPath(SX) without defining it (kiteNMPF.h:36); here it
-    // sets the path of the next createNLP()
+    // sets the tracked path: a live context is rebuilt (the path is part of the
+    // OCP), so computeControl and getPathFunction always agree on it
     void setPath(const FourierPath& path) {
         const int K = path.harmonics;
         if (K < 1 || K > KITE_PATH_MAX_HARMONICS || path.coef.size() != (size_t)3 * (2 * K + 1))
@@ -101,6 +102,7 @@ public:
             for (int j = 0; j < 2 * K + 1; ++j) cfg_.path_fourier[a][j] = path.coef[(size_t)a * (2 * K + 1) + j];
         cfg_.path_harmonics = K;
         for (int i = 0; i < 4; ++i) cfg_.path_q[i] = path.q[i];
+        if (ctx_) createNLP();
     }
     KiteNMPF(const kite_params& params, const kite_nmpc_config& cfg) : params_(params), cfg_(cfg) {}
     ~KiteNMPF() { kite_nmpc_destroy(ctx_); }

@@ -49,7 +49,8 @@ struct kite_nmpc_ctx {
     kite::RicConst ricc;
     // device copy of (rc, ricc) read by k_qp_ric; re-uploaded when the host copy changes
     void* dconst = nullptr;
-    std::vector<unsigned char> dconst_host;
+    std::vector<unsigned char> dconst_host;     // what dconst holds (empty: unknown)
+    std::vector<unsigned char> dconst_stage;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
                                    // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
@@ -203,8 +204,14 @@ int validate_config(const kite_nmpc_config& c) {
     for (int i = 0; i < 4; ++i) if (!(c.R[i] >= 0.0)) return KITE_EINVAL;
     if (!(c.W >= 0.0) || !(c.theta_flex > 0.0)) return KITE_EINVAL;
     if (c.qp_kernel < 0 || c.qp_kernel > 3) return KITE_EINVAL;
-    if (!(c.qp_soft_weight > 2.0 * 10.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;   // > 2 z0 (RIC_Z0)
-    if (!(c.qp_lm >= 0.0) || !std::isfinite(c.qp_lm)) return KITE_EINVAL;
+    // the multiple-shooting QP's soft-row weight and LM term (the condensed
+    // kernels 1 / 2 ignore both): soft_w > 2 z0 keeps the start point of
+    // every soft row dual feasible (z2 = soft_w - z0 > z0, RIC_Z0 = 20)
+    const int qk = c.qp_kernel ? c.qp_kernel : (c.N == 20 ? 2 : 3);
+    if (qk == 3) {
+        if (!(c.qp_soft_weight > 2.0 * 20.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;
+        if (!(c.qp_lm >= 0.0) || !std::isfinite(c.qp_lm)) return KITE_EINVAL;
+    }
     if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
     if (!(c.delay >= 0.0) || !std::isfinite(c.delay) || std::lround(c.delay / c.dt) > c.N) return KITE_EINVAL;
     if (c.delay > 0.0 && (c.delay_steps < 1 || c.delay_steps > 64)) return KITE_EINVAL;
@@ -277,8 +284,12 @@ int run_step(kite_nmpc_ctx* ctx) {
         std::memcpy(blob, &ctx->rc, sizeof(kite::RtiConst));
         std::memcpy(blob + roff, &ctx->ricc, sizeof(kite::RicConst));
         if (ctx->dconst_host.size() != sizeof(blob) || std::memcmp(ctx->dconst_host.data(), blob, sizeof(blob))) {
-            ctx->dconst_host.assign(blob, blob + sizeof(blob));
-            HIP_TRY(hipMemcpyAsync(ctx->dconst, ctx->dconst_host.data(), sizeof(blob), hipMemcpyHostToDevice, s));
+            // the host mirror is what the device holds: set only once the copy
+            // is enqueued (a failed copy leaves it empty, so the next step retries)
+            ctx->dconst_host.clear();
+            ctx->dconst_stage.assign(blob, blob + sizeof(blob));
+            HIP_TRY(hipMemcpyAsync(ctx->dconst, ctx->dconst_stage.data(), sizeof(blob), hipMemcpyHostToDevice, s));
+            ctx->dconst_host.swap(ctx->dconst_stage);
         }
         const auto* Cd = reinterpret_cast<const kite::RtiConst*>(ctx->dconst);
         const auto* Rd = reinterpret_cast<const kite::RicConst*>(static_cast<const unsigned char*>(ctx->dconst) + roff);

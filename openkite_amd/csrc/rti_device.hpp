@@ -110,6 +110,27 @@ __device__ __forceinline__ double nmax(double a, double b) { return (a != a || b
 struct OpNMax { __device__ double operator()(double a, double b) const { return nmax(a, b); } };
 
 __device__ __forceinline__ double row_sum16(double v) { return row_reduce16(v, OpAdd()); }
+// four row sums at once (transpose-reduce): v[q] -> sum of v[q] over the 16
+// lanes of each row, every lane.  Each butterfly level halves the values a lane
+// carries (xor 8: keep the pair of bit 3; xor 7 (row_half_mirror): keep one by
+// bit 2; xor 3, xor 1 (quad_perm): plain), so lane j ends with sum q = j >> 2,
+// broadcast back by row_newbcast: 10 DPP moves + 5 adds + 6 selects instead of
+// 4 x (8 DPP moves + 4 adds).  Every lane gets bitwise the same sums.
+// `hi8` / `hi4`: bit 3 / bit 2 of the lane's position in its row.
+__device__ __forceinline__ void row_sum16x4(double v[4], bool hi8, bool hi4) {
+    const double k0 = hi8 ? v[2] : v[0], k1 = hi8 ? v[3] : v[1];
+    const double s0 = hi8 ? v[0] : v[2], s1 = hi8 ? v[1] : v[3];
+    const double a0 = k0 + dpp_d<0x128>(s0);           // row_ror:8 = xor 8
+    const double a1 = k1 + dpp_d<0x128>(s1);
+    const double kb = hi4 ? a1 : a0, sb = hi4 ? a0 : a1;
+    double b = kb + dpp_d<0x141>(sb);                   // row_half_mirror = xor 7
+    b += dpp_d<0x1B>(b);                                // quad_perm [3,2,1,0] = xor 3
+    b += dpp_d<0xB1>(b);                                // quad_perm [1,0,3,2] = xor 1
+    v[0] = dpp_d<0x150>(b);                             // row_newbcast: lane 4q holds sum q
+    v[1] = dpp_d<0x154>(b);
+    v[2] = dpp_d<0x158>(b);
+    v[3] = dpp_d<0x15C>(b);
+}
 __device__ __forceinline__ double col_sum4(double v) { return col_reduce4(v, OpAdd()); }
 __device__ __forceinline__ double wave_sum(double v) { return col_reduce4(row_reduce16(v, OpAdd()), OpAdd()); }
 __device__ __forceinline__ double wave_max(double v) { return col_reduce4(row_reduce16(v, OpMax()), OpMax()); }

@@ -120,6 +120,8 @@ def lib():
             "orc_msqp_solve": (d, [dp, dp, i, i, dp, dp, i, dp, ip]),
             "orc_msqp_solve_pert": (d, [dp, dp, i, i, dp, dp, i, d, i, dp, ip]),
             "orc_set_ms_z0": (None, [d]),
+            "orc_set_ipm_z0": (None, [d]),
+            "orc_get_ipm_z0": (d, []),
             "orc_get_ms_z0": (d, []),
             "orc_msqp_build": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
             "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i, ip]),
@@ -294,6 +296,15 @@ def set_ms_z0(z0: float) -> float:
     L = lib()
     old = L.orc_get_ms_z0()
     L.orc_set_ms_z0(float(z0))
+    return old
+
+
+def set_ipm_z0(z0: float) -> float:
+    """Start multiplier of the oracle's condensed IPM (tools only; the GPU
+    kernels have their own constant IPM_Z0).  Returns the previous value."""
+    L = lib()
+    old = L.orc_get_ipm_z0()
+    L.orc_set_ipm_z0(float(z0))
     return old
 
 

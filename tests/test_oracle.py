@@ -192,24 +192,33 @@ def test_rti_is_deterministic_and_batch_invariant(kp, cfgv):
 
 
 def test_qp_sensitivity_envelope(kp, cfgv):
-    """Intrinsic sensitivity of the condensed QP (justifies RTI_TOL in
+    """Intrinsic sensitivity of the condensed QP (sets COND_ENVELOPE of
     test_gpu_parity.py): symmetric relative perturbations of H of 1e-15 --
     rounding-level differences between two fp64 implementations -- move the
-    oracle's own QP solution by more than 1e-8 on some instance and by less
-    than 1e-6 on all of them (cold start, instances of test_qp_kernels_vs_oracle)."""
-    from tests.test_gpu_parity import x0_batch
-    N, M, K = 20, 2, 16
-    x = x0_batch(16, offset=2000)
-    worst = 0.0
-    for b in range(16):
-        st, X, U, _ = ffi.prologue(kp, cfgv, N, M, x[b], np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
-        q = ffi.build_qp(kp, cfgv, N, M, X, U)
-        w0, k0 = ffi.qp_solve(q["H"], q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
-        E = np.random.default_rng(b).normal(size=q["H"].shape) * 1e-15
-        w1, k1 = ffi.qp_solve(q["H"] * (1 + (E + E.T) / 2), q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
-        assert k0 < 1e-8 and k1 < 1e-8
-        worst = max(worst, np.abs(w1 - w0).max() / max(1.0, np.abs(w0).max()))
-    assert 1e-8 < worst < 1e-6, worst
+    oracle's own frozen QP solution by up to ~2e-6 (cond(H) ~ 1e11): 64
+    closed-loop kites x 6 steps here, median ~1e-10; 1024 solves measured max
+    2.0e-6 at the former z0 = 10 and 6.9e-7 at z0 = 20."""
+    from tests.test_gpu_parity import COND_ENVELOPE, x0_batch
+    N, M, K, B = 20, 2, 16, 64
+    x = x0_batch(B, offset=2000)
+    X = np.zeros((B, N + 1, 15)); U = np.zeros((B, N, 4))
+    errs = []
+    for step in range(6):
+        for b in range(B):
+            st, Xp, Up, _ = ffi.prologue(kp, cfgv, N, M, x[b], X[b], U[b], warm=int(step > 0))
+            q = ffi.build_qp(kp, cfgv, N, M, Xp, Up)
+            w0, k0 = ffi.qp_solve(q["H"], q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
+            E = np.random.default_rng(1000 * b + step).normal(size=q["H"].shape) * 1e-15
+            w1, k1 = ffi.qp_solve(q["H"] * (1 + (E + E.T) / 2), q["h"], q["lb"], q["ub"], q["C"], q["c"], K)
+            if k0 < 1e-10 and k1 < 1e-10:
+                errs.append(np.abs(w1 - w0).max() / max(1.0, np.abs(w0).max()))
+        ffi.rti_step(kp, cfgv, N, M, K, x, X, U, warm=int(step > 0), nthreads=0)
+        x = X[:, 1, :].copy()
+    e = np.array(errs)
+    assert e.size >= 0.9 * B * 6
+    assert e.max() < COND_ENVELOPE and np.median(e) < 1e-8, (e.max(), np.median(e))
+    assert e.max() > 1e-9                              # the envelope is real: rounding moves solutions
+    print(f"condensed QP envelope: {e.size} frozen solves, median {np.median(e):.1e}, max {e.max():.1e}")
 
 
 def test_delay_compensation_prologue(kp):
