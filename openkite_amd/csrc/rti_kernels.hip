@@ -1344,6 +1344,10 @@ __device__ double lazy_row(const RtiConst& C, int b, int l, int k, int i, int si
 // closed loop's mean IPM iterations from 11.68 to 11.11 against z0 = 10,
 // profiles/r04_oracle_n20_z0_study.txt)
 constexpr double IPM_S0 = 0.1, IPM_Z0 = 20.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.995;
+// stalled IPM (oracle IPM_MU_FLOOR): complementarity exhausted (mu < 1e-20)
+// while a rounding floor of the stationarity residual keeps the test above the
+// freeze; continuing drives s, z to underflow and the Newton system to NaN
+constexpr double IPM_MU_FLOOR = 1e-20;
 __device__ __forceinline__ int pk(int i, int c) { return (i * (i + 1)) / 2 + c; }
 
 // row of element e in a row-wise packed lower triangle
@@ -1659,7 +1663,7 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
     iters = C.K;
     for (int it = 0; it < C.K; ++it) {
         const double mu = residuals();
-        if (resid < IPM_FREEZE || resid != resid) { iters = it; break; }   // converged, or poisoned
+        if (resid < IPM_FREEZE || resid != resid || mu < IPM_MU_FLOOR) { iters = it; break; }   // converged, poisoned or stalled
         // sigma = z/s and the normal matrix H + A' Sigma A into Lp
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
