@@ -55,11 +55,29 @@ def parse(argv=None):
                     help="RK4 + sensitivities in fp32, QP fp64 (BASELINE configs[3] mixed precision)")
     ap.add_argument("--ekf", action="store_true",
                     help="fuse the EKF estimate (kiteEKF.cpp) before every RTI step (BASELINE configs[4])")
+    ap.add_argument("--wind-sweep", type=float, default=0.0, metavar="VMAX",
+                    help="wind-field sweep: a seeded constant world-frame wind per instance, horizontal speed "
+                         "up to VMAX m/s (kite_nmpc_set_wind; a build extension, the reference model has no "
+                         "wind); 0 = no wind, the reference model")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--latency-steps", type=int, default=1000,
                     help="warm single-kite steps of the single-thread CPU latency (BASELINE config 1)")
     return ap.parse_args(argv)
+
+
+def synthetic_wind(B, offset, vmax):
+    """Wind-field sweep: per global instance a seeded world-frame wind, horizontal
+    speed U(0, vmax) in a uniform direction, vertical U(-0.2, 0.2) vmax (None for
+    vmax = 0: no wind)."""
+    if vmax <= 0.0:
+        return None
+    w = np.zeros((B, 3))
+    for b in range(B):
+        rng = np.random.default_rng(77_000_000 + offset + b)
+        ang, sp = rng.uniform(0.0, 2 * math.pi), rng.uniform(0.0, vmax)
+        w[b] = [sp * math.cos(ang), sp * math.sin(ang), rng.uniform(-0.2, 0.2) * vmax]
+    return w
 
 
 def synthetic_x0(B, offset, ctx):
@@ -138,7 +156,7 @@ def host_cpu_info():
                 omp_num_threads=int(omp) if omp and omp.isdigit() else None)
 
 
-def cpu_baseline(args, x0_host, budget_s):
+def cpu_baseline(args, x0_host, budget_s, wind=None):
     """The CPU oracle (oracle/kite_oracle.cpp, OpenMP over instances) on a
     bounded sample of the same workload: same instances, cold start + warm
     closed-loop steps, same N/M/K; plus the single-thread, batch-1 latency
@@ -154,12 +172,13 @@ def cpu_baseline(args, x0_host, budget_s):
     N = args.horizon
     S = min(x0_host.shape[0], 64 * threads)
     x = x0_host[:S].copy()
+    ws = None if wind is None else wind[:S]
     X = np.zeros((S, N + 1, 15)); U = np.zeros((S, N, 4))
-    ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=0, nthreads=threads)
+    ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=0, nthreads=threads, wind=ws)
     x = X[:, 1, :].copy()
     steps, t0 = 0, time.perf_counter()
     while True:
-        ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=1, nthreads=threads)
+        ffi.rti_step(kp, cfgv, N, args.substeps, args.qp_iters, x, X, U, warm=1, nthreads=threads, wind=ws)
         x = X[:, 1, :].copy()
         steps += 1
         el = time.perf_counter() - t0
@@ -193,8 +212,11 @@ def cpu_baseline(args, x0_host, budget_s):
 
 
 def run_config_tag(args):
-    return dict(batch=args.batch, N=args.horizon, M=args.substeps, K=args.qp_iters,
-                fp32_sens=bool(args.fp32_sens), ekf=bool(args.ekf), qp_kernel=args.qp_kernel)
+    tag = dict(batch=args.batch, N=args.horizon, M=args.substeps, K=args.qp_iters,
+               fp32_sens=bool(args.fp32_sens), ekf=bool(args.ekf), qp_kernel=args.qp_kernel)
+    if args.wind_sweep > 0.0:
+        tag["wind_sweep"] = args.wind_sweep
+    return tag
 
 
 def pmc_traffic(names, cfg_tag):
@@ -331,6 +353,9 @@ def main():
     offset, count = shard(world * B, world, rank)      # weak scaling: B instances per GPU
     assert count == B
     x0_host = synthetic_x0(B, offset, ctx)
+    wind = synthetic_wind(B, offset, args.wind_sweep)
+    if wind is not None:
+        ctx.set_wind(wind)
     pub = Publisher(B, dev, world) if distributed and not args.no_allgather else None
     loop = FleetLoop(GpuStepper(ctx), torch.from_numpy(x0_host).to(dev), N, cfg.dt, ekf=args.ekf,
                      covariances=ok.ekf_default_covariances() if args.ekf else None, publisher=pub)
@@ -387,14 +412,16 @@ def main():
                              f"events on the step stream); traffic = HBM bytes per launch from {tsrc}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, x0_host, args.cpu_seconds)
+            cpu = cpu_baseline(args, x0_host, args.cpu_seconds, wind)
         # beside the CPU baseline only (the profiled runs pass --no-cpu-baseline and
         # must see the batch launches alone)
         lat1 = gpu_single_kite_latency(args, ok, x0_host[:1]) if world == 1 and not args.no_cpu_baseline else None
         workload = (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
                     + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
                     + (" + fused EKF (BASELINE configs[4])" if args.ekf else
-                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens else ""))
+                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens and wind is None else "")
+                    + (f", wind-field sweep |W_h| <= {args.wind_sweep} m/s per instance (build extension)"
+                       if wind is not None else ""))
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -411,7 +438,7 @@ def main():
             "config": {"workload": workload, "ekf": bool(args.ekf),
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
-                       "allgather": pub is not None,
+                       "allgather": pub is not None, "wind_sweep_mps": args.wind_sweep,
                        "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -126,11 +126,20 @@ public:
         if (ctx_) kite_check(kite_nmpc_set_reference_velocity(ctx_, v), "setReferenceVelocity");
     }
 
+    // constant world-frame wind of the prediction model, m/s (build extension,
+    // kite_nmpc_set_wind: the reference model has no wind, kite.cpp:196); kept
+    // across createNLP
+    void setWind(double wx, double wy, double wz) {
+        wind_[0] = wx; wind_[1] = wy; wind_[2] = wz;
+        if (ctx_) kite_check(kite_nmpc_set_wind(ctx_, wind_), "setWind");
+    }
+
     // ---- lifecycle (kiteNMPF.h:37-41) ---------------------------------------
     void createNLP() {
         kite_nmpc_destroy(ctx_);
         ctx_ = nullptr;
         kite_check(kite_nmpc_create(&params_, &cfg_, 1, &ctx_), "createNLP");
+        kite_check(kite_nmpc_set_wind(ctx_, wind_), "createNLP");
         warm_ = false;
     }
     void enableWarmStart() { warm_ = true; }
@@ -229,6 +238,7 @@ private:
     kite_nmpc_config cfg_;
     kite_nmpc_ctx* ctx_ = nullptr;
     bool warm_ = false;
+    double wind_[3] = {0.0, 0.0, 0.0};
     std::vector<double> traj_, ctrl_;
     double u0_[4] = {0, 0, 0, 0};
     kite_mpc_diagnostic diag_{};

@@ -35,11 +35,12 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 4   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+#define KITE_NMPC_API_VERSION 5   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
                                       qp_kernel 3 (multiple-shooting QP, Riccati IPM);
                                    3: kite_nmpc_config gained path_harmonics, path_fourier
                                       (arbitrary closed paths); delay_steps default 16;
-                                   4: kite_nmpc_state_bound_stats (no config change) */
+                                   4: kite_nmpc_state_bound_stats (no config change);
+                                   5: kite_nmpc_set_wind (no config change) */
 #define KITE_PATH_MAX_HARMONICS 8 /* Fourier path: harmonics per axis              */
 
 /* ---- error codes ------------------------------------------------------ */
@@ -185,6 +186,16 @@ int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* 
 int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref);
 /* disableWarmStart (kiteNMPF.h:40): the next step cold-starts.              */
 int kite_nmpc_reset(kite_nmpc_ctx* ctx);
+/* Wind-field sweeps (the batch dimension of BASELINE north_star): a constant
+ * world-frame wind per instance, wind[3 b + i] in m/s (B x 3), or NULL for
+ * none.  Build extension: the reference model has no wind (kite.cpp:196
+ * "@todo: add wind"); with wind the RTI model's aerodynamics see the
+ * air-relative velocity v - q^-1 W q (kite_model.hpp), used by every step's
+ * prediction (cold start, delay compensation, sensitivities, defects).  The
+ * item-wise model entry points (dynamics, jacobian, predict, rk4_sens) and
+ * the EKF keep the reference model.  All-zero wind is the reference model
+ * bit for bit.  Non-finite entries: KITE_EINVAL.                            */
+int kite_nmpc_set_wind(kite_nmpc_ctx* ctx, const double* wind);
 /* Run on this HIP stream (hipStream_t as void*).  NULL is the HIP null
  * (legacy default) stream -- the stream PyTorch's default stream maps to.
  * A new context runs on a private non-blocking stream; restore it with

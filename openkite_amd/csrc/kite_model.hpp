@@ -237,27 +237,42 @@ __host__ __device__ __forceinline__ V3<T> rot_world(T w, const V3<T>& u, T ww_uu
 
 // ---------------------------------------------------------------------------
 // kite ODE  x = [v(3) w(3) r(3) q(4)], u = [T dE dR]  -> f[13]
+//
+// WIND (build extension for wind-field batch sweeps; the reference model has
+// no wind, kite.cpp:196 "@todo: add wind"): a constant world-frame wind W
+// (wnd[0..2], m/s) makes the aerodynamics -- airspeed, angles, dynamic
+// pressure, the rate-damping terms -- see the air-relative body velocity
+// v_a = v - q^-1 (x) [0,W] (x) q, while gravity, the tether and the kinematics
+// keep the inertial v.  WIND = false is the reference model, instruction for
+// instruction.
 // ---------------------------------------------------------------------------
-template <class T>
-__host__ __device__ __forceinline__ void kite_rhs(const ModelConst& P, const T* x, const T* u, T* f) {
+template <class T, bool WIND = false>
+__host__ __device__ __forceinline__ void kite_rhs(const ModelConst& P, const T* x, const T* u, T* f,
+                                                  const double* wnd = nullptr) {
     const V3<T> v{x[0], x[1], x[2]};
     const V3<T> w{x[3], x[4], x[5]};
     const V3<T> r{x[6], x[7], x[8]};
     const T qw = x[9];
     const V3<T> qu{x[10], x[11], x[12]};
     const T thr = u[0], dE = u[1], dR = u[2];
+    V3<T> va = v;
+    if constexpr (WIND) {
+        const T wwuu = qw * qw - dot3(qu, qu);
+        const V3<T> Wb = rot_body(qw, qu, wwuu, V3<T>{T(wnd[0]), T(wnd[1]), T(wnd[2])});
+        va = V3<T>{v.x - Wb.x, v.y - Wb.y, v.z - Wb.z};
+    }
 
     // airspeed, angles (kite.cpp:197-202)
-    const T V2 = dot3(v, v);
+    const T V2 = dot3(va, va);
     const T V = dsqrt(V2);
-    const T sb = v.y * rcp(V + 1e-4);              // sin(ss)
+    const T sb = va.y * rcp(V + 1e-4);             // sin(ss)
     const T cb = dsqrt(1.0 - sb * sb);             // cos(ss) >= 0
     const T ss = dasin(sb, cb);
-    const T ax = v.x + 1e-4;
-    const T r2a = ax * ax + v.z * v.z;
-    const T aoa = datan2(v.z, ax, r2a);
+    const T ax = va.x + 1e-4;
+    const T r2a = ax * ax + va.z * va.z;
+    const T aoa = datan2(va.z, ax, r2a);
     const T ira = rcp(dsqrt(r2a));
-    const T ca = ax * ira, sa = v.z * ira;          // cos/sin(aoa)
+    const T ca = ax * ira, sa = va.z * ira;         // cos/sin(aoa)
     const T qbar = P.half_rho * V2;
     const T qS = qbar * P.S;
 

@@ -52,6 +52,8 @@ struct kite_nmpc_ctx {
     std::vector<unsigned char> dconst_host;     // what dconst holds (empty: unknown)
     std::vector<unsigned char> dconst_stage;
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
+    double* wind = nullptr;        // per-kite world-frame wind B x 3 (kite_nmpc_set_wind)
+    bool has_wind = false;         // a nonzero wind is set: the WIND kernels run
     double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
                                    // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
     // scratch for the model-level entry points
@@ -245,7 +247,7 @@ int ensure_scratch(kite_nmpc_ctx* ctx, size_t bytes) {
 void free_ctx(kite_nmpc_ctx* ctx) {
     double** bufs[] = {&ctx->X, &ctx->U, &ctx->x0, &ctx->AB, &ctx->DEF, &ctx->Hs, &ctx->hs,
                        &ctx->Cr, &ctx->cl, &ctx->cu, &ctx->hmax, &ctx->u0, &ctx->diag, &ctx->kkt,
-                       &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb, &ctx->wstep};
+                       &ctx->scratch, &ctx->Htl, &ctx->Hab, &ctx->Hbb, &ctx->wstep, &ctx->wind};
     for (double** p : bufs) if (*p) { (void)hipFree(*p); *p = nullptr; }
     if (ctx->dconst) { (void)hipFree(ctx->dconst); ctx->dconst = nullptr; }
     if (ctx->status) { (void)hipFree(ctx->status); ctx->status = nullptr; }
@@ -266,9 +268,11 @@ int run_step(kite_nmpc_ctx* ctx) {
     if (ctx->ring_used < ctx->ring_cap) ev = &ctx->ring[(size_t)ctx->ring_used++ * 5];
     else if (ctx->cfg.timing) ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
-    HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, ctx->x0, ctx->X, ctx->U, ctx->status, s));
+    const double* wind = ctx->has_wind ? ctx->wind : nullptr;
+    HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, ctx->x0, ctx->X, ctx->U, ctx->status,
+                                  wind, s));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, s));
+    HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, wind, s));
     if (ev) HIP_TRY(hipEventRecord(ev[2], s));
     if (!ctx->ric)
         HIP_TRY(kite::launch_condense(ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, ctx->Hs, ctx->hs, ctx->Cr,
@@ -545,6 +549,25 @@ int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref) {
 int kite_nmpc_reset(kite_nmpc_ctx* ctx) {
     if (!ctx) return KITE_EINVAL;
     ctx->warm = false;
+    return KITE_OK;
+}
+
+int kite_nmpc_set_wind(kite_nmpc_ctx* ctx, const double* wind) {
+    if (!ctx) return KITE_EINVAL;
+    bool any = false;
+    if (wind) {
+        for (size_t e = 0; e < (size_t)ctx->B * 3; ++e) {
+            if (!std::isfinite(wind[e])) return KITE_EINVAL;
+            any = any || wind[e] != 0.0;
+        }
+    }
+    if (!any) { ctx->has_wind = false; return KITE_OK; }   // the reference model
+    if (!ctx->wind) HIP_TRY(hipMalloc(&ctx->wind, (size_t)ctx->B * 3 * sizeof(double)));
+    // ordered with the steps on the context stream (the host array may be
+    // reused as soon as this returns: synchronous on that stream)
+    HIP_TRY(hipMemcpyAsync(ctx->wind, wind, (size_t)ctx->B * 3 * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->has_wind = true;
     return KITE_OK;
 }
 

@@ -48,9 +48,11 @@ __device__ double closest_point_dev(const RtiConst& C, double px, double py, dou
     return th;
 }
 
-// primal RK4 of the augmented 15-state model, M substeps of length h
+// primal RK4 of the augmented 15-state model, M substeps of length h (WIND:
+// the constant world-frame wind wnd[0..2] of this kite, kite_model.hpp)
+template <bool WIND = false>
 __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* u, double h, int M,
-                           double* xo) {
+                           double* xo, const double* wnd = nullptr) {
     double x[NX], xs[NX], acc[NX], k[NK];
 #pragma unroll
     for (int i = 0; i < NX; ++i) x[i] = x0[i];
@@ -59,7 +61,7 @@ __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* 
         for (int i = 0; i < NX; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
 #pragma unroll 1
         for (int st = 0; st < 4; ++st) {
-            kite_rhs<double>(P, xs, u, k);
+            kite_rhs<double, WIND>(P, xs, u, k, wnd);
             const double kt = xs[14], kth = u[3];   // theta' = thetadot, thetadot' = Uv
             const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
             const double wn = (st < 2) ? 0.5 * h : h;
@@ -86,7 +88,7 @@ __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* 
 __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
                                                  const double* __restrict__ x0in,
                                                  double* __restrict__ X, double* __restrict__ U,
-                                                 int32_t* __restrict__ status) {
+                                                 int32_t* __restrict__ status, const double* __restrict__ wind) {
     __shared__ double sx0[NX];
     __shared__ double sUv[KITE_NMAX];
     __shared__ int sWarm;
@@ -120,7 +122,8 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
             // thetadot from the previous trajectory at t0 + delay
             const double up[NU] = {Ub[0], Ub[1], Ub[2], 0.0};
             double xp[NX];
-            rk4_primal(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp);
+            if (wind) rk4_primal<true>(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp, wind + 3 * b);
+            else rk4_primal(P, x0, up, C.delay / C.delay_steps, C.delay_steps, xp);
             for (int i = 0; i < 13; ++i) x0[i] = xp[i];
             x0[13] = Xb[C.delay_node * NX + 13];
             x0[14] = Xb[C.delay_node * NX + 14];
@@ -133,7 +136,10 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
             for (int k = 0; k < N; ++k)
                 for (int j = 0; j < NU; ++j) Ub[k * NU + j] = 0.5 * (C.lbu[j] + C.ubu[j]);
             for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
-            for (int k = 0; k < N; ++k) rk4_primal(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX]);
+            for (int k = 0; k < N; ++k) {
+                if (wind) rk4_primal<true>(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX], wind + 3 * b);
+                else rk4_primal(P, &Xb[k * NX], &Ub[k * NU], C.h, C.M, &Xb[(k + 1) * NX]);
+            }
             for (int k = 0; k < N; ++k) sUv[k] = Ub[k * NU + 3];
         } else if (!C.shift) {
             for (int k = 0; k < N; ++k) sUv[k] = Ub[k * NU + 3];
@@ -208,11 +214,13 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
 constexpr int RK2_T = 64;                 // threads per block = 8 instances x 8 direction pairs
 // DT: Dual2 (fp64) or DualF2 (fp32 sensitivities, config sens_fp32 = 1; the
 // defects then come from k_defects in fp64), ST its scalar
-template <class DT, class ST>
+// WIND: per-kite world-frame wind wind[3 b .. 3 b + 2] (wind-field sweeps)
+template <class DT, class ST, bool WIND = false>
 __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int N, int M, double h,
                                                         const double* __restrict__ X,
                                                         const double* __restrict__ U,
-                                                        double* __restrict__ AB, double* __restrict__ DEF) {
+                                                        double* __restrict__ AB, double* __restrict__ DEF,
+                                                        const double* __restrict__ wind = nullptr) {
     const int d = threadIdx.x & 7;
     const int b = blockIdx.x * (RK2_T / 8) + (threadIdx.x >> 3);
     const int k = blockIdx.y;
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
         for (int i = 0; i < NK; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
 #pragma unroll 1
         for (int st = 0; st < 4; ++st) {
-            kite_rhs<DT>(P, xs, u, kv);
+            kite_rhs<DT, WIND>(P, xs, u, kv, WIND ? wind + 3 * b : nullptr);
             const ST wa = (st == 0 || st == 3) ? hs / ST(6) : hs / ST(3);
             const ST wn = (st < 2) ? ST(0.5) * hs : hs;
 #pragma unroll
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
 // interval): the right-hand side of the QP when the sensitivities run in fp32
 __global__ __launch_bounds__(64, 2) void k_defects(ModelConst P, int B, int N, int M, double h,
                                                  const double* __restrict__ X, const double* __restrict__ U,
-                                                 double* __restrict__ DEF) {
+                                                 double* __restrict__ DEF, const double* __restrict__ wind) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= B * N) return;
     const int b = g / N, k = g % N;
@@ -274,7 +282,8 @@ __global__ __launch_bounds__(64, 2) void k_defects(ModelConst P, int B, int N, i
     double x0[NX], u4[NU], xo[NX];
     for (int i = 0; i < NX; ++i) x0[i] = xk[i];
     for (int j = 0; j < NU; ++j) u4[j] = uk[j];
-    rk4_primal(P, x0, u4, h, M, xo);
+    if (wind) rk4_primal<true>(P, x0, u4, h, M, xo, wind + 3 * b);
+    else rk4_primal(P, x0, u4, h, M, xo);
     double* df = DEF + ((size_t)b * N + k) * NK;
     for (int i = 0; i < NK; ++i) df[i] = xo[i] - xk[NX + i];
 }
@@ -1903,20 +1912,29 @@ __global__ __launch_bounds__(64, 2) void k_closest_point(RtiConst C, int count, 
 // launch wrappers
 // ---------------------------------------------------------------------------
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
-                           double* X, double* U, int32_t* status, hipStream_t s) {
-    hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status);
+                           double* X, double* U, int32_t* status, const double* wind, hipStream_t s) {
+    hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status, wind);
     return hipGetLastError();
 }
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
-                           double* AB, double* DEF, hipStream_t s) {
+                           double* AB, double* DEF, const double* wind, hipStream_t s) {
     const dim3 grid2((B + RK2_T / 8 - 1) / (RK2_T / 8), C.N);
     if (C.sens_fp32) {
-        hipLaunchKernelGGL((k_rk4_sens2<DualF2, float>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB,
-                           DEF);
-        hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF);
+        if (wind)
+            hipLaunchKernelGGL((k_rk4_sens2<DualF2, float, true>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X,
+                               U, AB, DEF, wind);
+        else
+            hipLaunchKernelGGL((k_rk4_sens2<DualF2, float>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U,
+                               AB, DEF, nullptr);
+        hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF,
+                           wind);
     } else {
-        hipLaunchKernelGGL((k_rk4_sens2<Dual2, double>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U, AB,
-                           DEF);
+        if (wind)
+            hipLaunchKernelGGL((k_rk4_sens2<Dual2, double, true>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X,
+                               U, AB, DEF, wind);
+        else
+            hipLaunchKernelGGL((k_rk4_sens2<Dual2, double>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X, U,
+                               AB, DEF, nullptr);
     }
     return hipGetLastError();
 }
@@ -2014,7 +2032,7 @@ hipError_t launch_rk4_sens_items(const ModelConst& P, int sens_fp32, int count, 
     hipLaunchKernelGGL(k_sens_items_stage, dim3((count * 2 * NX + 63) / 64), dim3(64), 0, s, count, x, X2);
     RtiConst C{};
     C.N = 1; C.M = M; C.h = h; C.sens_fp32 = sens_fp32;
-    hipError_t e = launch_rk4_sens(P, C, count, X2, u, AB, DEF, s);
+    hipError_t e = launch_rk4_sens(P, C, count, X2, u, AB, DEF, nullptr, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sens_items_expand, dim3((count * NX + 63) / 64), dim3(64), 0, s, count, M, h, x, u, AB, DEF,
                        xo, A, Bm);

@@ -65,10 +65,12 @@ hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, const RtiConst* C
                          int32_t* status, double* kkt, int32_t* iters, int32_t* iters_acc, const int32_t* order,
                          double* ws, hipStream_t s);
 
+// wind: per-kite constant world-frame wind (B x 3, m/s) or nullptr (the
+// reference model, no wind; kite_model.hpp kite_rhs<T, WIND>)
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
-                           double* X, double* U, int32_t* status, hipStream_t s);
+                           double* X, double* U, int32_t* status, const double* wind, hipStream_t s);
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
-                           double* AB, double* DEF, hipStream_t s);
+                           double* AB, double* DEF, const double* wind, hipStream_t s);
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
                            const double* DEF, double* Hs, double* hs, double* Cr, double* cl, double* cu,
                            double* hmax, int tiled, double* Htl, double* Hab, double* Hbb, hipStream_t s);

@@ -134,6 +134,7 @@ _SIGNATURES = {
     "kite_nmpc_set_bounds": (ctypes.c_int, [ctypes.c_void_p, _DP, _DP, _DP, _DP]),
     "kite_nmpc_set_reference_velocity": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     "kite_nmpc_reset": (ctypes.c_int, [ctypes.c_void_p]),
+    "kite_nmpc_set_wind": (ctypes.c_int, [ctypes.c_void_p, _DP]),
     "kite_nmpc_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "kite_nmpc_use_own_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "kite_nmpc_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
@@ -287,6 +288,16 @@ class BatchNMPC:
 
     def reset(self):
         _check(lib().kite_nmpc_reset(self._h), "reset")
+
+    def set_wind(self, wind=None):
+        """Per-kite constant world-frame wind, (B, 3) m/s, for wind-field sweeps
+        (kite_nmpc_set_wind; None or all zero = the reference model, which has
+        no wind)."""
+        if wind is None:
+            _check(lib().kite_nmpc_set_wind(self._h, None), "set_wind")
+            return
+        w = np.ascontiguousarray(np.asarray(wind, dtype=np.float64).reshape(self.batch, 3))
+        _check(lib().kite_nmpc_set_wind(self._h, w.ctypes.data_as(_DP)), "set_wind")
 
     def set_stream(self, stream_ptr: int):
         """Run on this hipStream_t (int handle; 0 = the HIP null stream, which is

@@ -119,6 +119,8 @@ def lib():
             "orc_prologue": (i, [dp, dp, i, i, dp, i, i, dp, dp, dp]),
             "orc_msqp_solve": (d, [dp, dp, i, i, dp, dp, i, dp, ip]),
             "orc_msqp_solve_pert": (d, [dp, dp, i, i, dp, dp, i, d, i, dp, ip]),
+            "orc_set_wind": (None, [dp]),
+            "orc_set_wind_batch": (None, [dp, i]),
             "orc_set_ms_z0": (None, [d]),
             "orc_set_ipm_z0": (None, [d]),
             "orc_get_ipm_z0": (d, []),
@@ -324,19 +326,31 @@ def prologue(kp, cfgv, N, M, x0, X, U, warm, shift=1):
     return st, X, U, x0o
 
 
-def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0, iters=None):
+def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0, iters=None, wind=None):
     """Batched RTI step.  x0 (B,15); X (B,N+1,15) and U (B,N,4) updated in place.
     iters (optional int32 array of B): QP interior-point iterations per kite (the
-    condensed form counts the last re-solve only)."""
+    condensed form counts the last re-solve only).  wind (optional (B,3)): per-kite
+    world-frame wind (build extension; None = the reference model)."""
     B = x0.shape[0]
     assert X.shape == (B, N + 1, 15) and U.shape == (B, N, 4)
     assert X.dtype == np.float64 and U.dtype == np.float64 and X.flags["C_CONTIGUOUS"] and U.flags["C_CONTIGUOUS"]
     u0 = np.zeros((B, 4)); diag = np.zeros((B, 6)); status = np.zeros(B, dtype=np.int32)
     ip = ctypes.POINTER(ctypes.c_int32)
-    lib().orc_rti_step(_p(kp), _p(cfgv), N, M, K, B, int(warm), int(shift), _p(_f64(x0)), _p(X), _p(U),
-                       _p(u0), _p(diag), status.ctypes.data_as(ip), int(nthreads),
-                       None if iters is None else iters.ctypes.data_as(ip))
+    wv = None if wind is None else _f64(np.asarray(wind, dtype=np.float64).reshape(B, 3))
+    lib().orc_set_wind_batch(None if wv is None else _p(wv), B)
+    try:
+        lib().orc_rti_step(_p(kp), _p(cfgv), N, M, K, B, int(warm), int(shift), _p(_f64(x0)), _p(X), _p(U),
+                           _p(u0), _p(diag), status.ctypes.data_as(ip), int(nthreads),
+                           None if iters is None else iters.ctypes.data_as(ip))
+    finally:
+        lib().orc_set_wind_batch(None, 0)
     return u0, diag, status
+
+
+def set_wind(w3):
+    """World-frame wind of this thread's single-kite oracle calls (rhs, rk4,
+    rk4_sens, prologue, ...); None = no wind (the reference model)."""
+    lib().orc_set_wind(None if w3 is None else _p(_f64(np.asarray(w3, dtype=np.float64).reshape(3))))
 
 
 def traj_cost(cfgv, N, X, U):
