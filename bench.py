@@ -58,7 +58,8 @@ def parse(argv=None):
     ap.add_argument("--wind-sweep", type=float, default=0.0, metavar="VMAX",
                     help="wind-field sweep: a seeded constant world-frame wind per instance, horizontal speed "
                          "up to VMAX m/s (kite_nmpc_set_wind; a build extension, the reference model has no "
-                         "wind); 0 = no wind, the reference model")
+                         "wind); 0 = no wind, the reference model.  The synthetic ~4.5 m/s kites stay in their "
+                         "envelope over a long closed loop up to ~0.5 m/s (DESIGN 2.1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--latency-steps", type=int, default=1000,
