@@ -127,6 +127,8 @@ def lib():
             "orc_get_ms_z0": (d, []),
             "orc_msqp_build": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
             "orc_rti_step": (None, [dp, dp, i, i, i, i, i, i, dp, dp, dp, dp, dp, ip, i, ip]),
+            "orc_set_sqp": (None, [d, i]),
+            "orc_sqp_step": (None, [dp, dp, i, i, i, i, i, i, i, d, dp, dp, dp, dp, dp, ip, i, ip, dp]),
             "orc_traj_cost": (d, [dp, i, dp, dp]),
             "orc_cheb_points": (None, [i, dp]),
             "orc_cheb_D": (None, [i, dp]),
@@ -345,6 +347,28 @@ def rti_step(kp, cfgv, N, M, K, x0, X, U, warm, shift=1, nthreads=0, iters=None,
     finally:
         lib().orc_set_wind_batch(None, 0)
     return u0, diag, status
+
+
+def sqp_step(kp, cfgv, N, M, K, x0, X, U, warm, maxit, tol, shift=1, nthreads=0, wind=None):
+    """Gauss-Newton SQP to convergence at one sampling instant (orc_sqp_step):
+    the RTI step, then re-linearisations at the same processed measurement with
+    the theta box fixed at it, until the full step (scaled inf-norm) is below
+    tol or maxit iterations.  Returns u0, diag, status, sqp iterations, last step."""
+    B = x0.shape[0]
+    assert X.shape == (B, N + 1, 15) and U.shape == (B, N, 4)
+    assert X.dtype == np.float64 and U.dtype == np.float64 and X.flags["C_CONTIGUOUS"] and U.flags["C_CONTIGUOUS"]
+    u0 = np.zeros((B, 4)); diag = np.zeros((B, 6)); status = np.zeros(B, dtype=np.int32)
+    its = np.zeros(B, dtype=np.int32); step = np.zeros(B)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    wv = None if wind is None else _f64(np.asarray(wind, dtype=np.float64).reshape(B, 3))
+    lib().orc_set_wind_batch(None if wv is None else _p(wv), B)
+    try:
+        lib().orc_sqp_step(_p(kp), _p(cfgv), N, M, K, B, int(warm), int(shift), int(maxit), float(tol),
+                           _p(_f64(x0)), _p(X), _p(U), _p(u0), _p(diag), status.ctypes.data_as(ip),
+                           int(nthreads), its.ctypes.data_as(ip), _p(step))
+    finally:
+        lib().orc_set_wind_batch(None, 0)
+    return u0, diag, status, its, step
 
 
 def set_wind(w3):
