@@ -259,8 +259,10 @@ void free_ctx(kite_nmpc_ctx* ctx) {
     if (ctx->own_stream) { (void)hipStreamDestroy(ctx->own_stream); ctx->own_stream = nullptr; }
 }
 
-// Runs the four RTI kernels on ctx->stream.  Inputs: ctx->x0 filled.
-int run_step(kite_nmpc_ctx* ctx) {
+// Runs the RTI kernels on ctx->stream.  x0: B x 15 measured states in device
+// memory (ctx->x0, or the caller's buffer for kite_nmpc_step_device: the
+// prologue reads it in stream order, as a copy would).
+int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     hipStream_t s = ctx->stream;
     const int B = ctx->B;
     // events: the last-step set (cfg.timing) or the next slot of the ring
@@ -269,7 +271,7 @@ int run_step(kite_nmpc_ctx* ctx) {
     else if (ctx->cfg.timing) ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
-    HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, ctx->x0, ctx->X, ctx->U, ctx->status,
+    HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, x0, ctx->X, ctx->U, ctx->status,
                                   wind, s));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, wind, s));
@@ -596,14 +598,10 @@ int kite_nmpc_step_device(kite_nmpc_ctx* ctx, const double* d_x0, double* d_u0, 
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t B = ctx->B, N = ctx->cfg.N;
     hipStream_t s = ctx->stream;
-    HIP_TRY(hipMemcpyAsync(ctx->x0, d_x0, B * 15 * sizeof(double), hipMemcpyDeviceToDevice, s));
-    int rc = run_step(ctx);
+    int rc = run_step(ctx, d_x0);
     if (rc) return rc;
-    if (d_u0) HIP_TRY(hipMemcpyAsync(d_u0, ctx->u0, B * 4 * sizeof(double), hipMemcpyDeviceToDevice, s));
-    if (d_traj) HIP_TRY(hipMemcpyAsync(d_traj, ctx->X, B * (N + 1) * 15 * sizeof(double), hipMemcpyDeviceToDevice, s));
-    if (d_ctrl) HIP_TRY(hipMemcpyAsync(d_ctrl, ctx->U, B * N * 4 * sizeof(double), hipMemcpyDeviceToDevice, s));
-    if (d_diag) HIP_TRY(hipMemcpyAsync(d_diag, ctx->diag, B * 6 * sizeof(double), hipMemcpyDeviceToDevice, s));
-    if (d_status) HIP_TRY(hipMemcpyAsync(d_status, ctx->status, B * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(kite::launch_publish((int)B, (int)N, ctx->u0, ctx->X, ctx->U, ctx->diag, ctx->status, d_u0, d_traj,
+                                 d_ctrl, d_diag, d_status, s));
     return KITE_OK;
 }
 
@@ -615,7 +613,7 @@ int kite_nmpc_step(kite_nmpc_ctx* ctx, const double* x0, double* u0_out, double*
     const size_t B = ctx->B, N = ctx->cfg.N;
     hipStream_t s = ctx->stream;
     HIP_TRY(hipMemcpyAsync(ctx->x0, x0, B * 15 * sizeof(double), hipMemcpyHostToDevice, s));
-    int rc = run_step(ctx);
+    int rc = run_step(ctx, ctx->x0);
     if (rc) return rc;
     if (u0_out) HIP_TRY(hipMemcpyAsync(u0_out, ctx->u0, B * 4 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (traj_out) HIP_TRY(hipMemcpyAsync(traj_out, ctx->X, B * (N + 1) * 15 * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -2006,6 +2006,45 @@ __global__ __launch_bounds__(1024) void k_qp_order(int B, int K, const int32_t* 
     __syncthreads();
     for (int b = t; b < B; b += 1024) order[atomicAdd(&cnt[key(b)], 1)] = b;
 }
+// kite_nmpc_step_device's outputs in one launch instead of one copy each:
+// blockIdx.y picks the array (u0, traj, ctrl, diag as doubles, status as
+// 32-bit words), a grid-stride loop copies it (a null destination is skipped)
+struct PublishArgs {
+    const void* src[5];
+    void* dst[5];
+    size_t words[5];      // 8-byte words (status: 4-byte words)
+};
+__global__ __launch_bounds__(256) void k_publish(PublishArgs a) {
+    const int y = blockIdx.y;
+    if (!a.dst[y]) return;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (y < 4) {
+        const double* __restrict__ src = static_cast<const double*>(a.src[y]);
+        double* __restrict__ dst = static_cast<double*>(a.dst[y]);
+        for (; i < a.words[y]; i += stride) dst[i] = src[i];
+    } else {
+        const int32_t* __restrict__ src = static_cast<const int32_t*>(a.src[y]);
+        int32_t* __restrict__ dst = static_cast<int32_t*>(a.dst[y]);
+        for (; i < a.words[y]; i += stride) dst[i] = src[i];
+    }
+}
+hipError_t launch_publish(int B, int N, const double* u0, const double* X, const double* U, const double* diag,
+                          const int32_t* status, double* d_u0, double* d_traj, double* d_ctrl, double* d_diag,
+                          int32_t* d_status, hipStream_t s) {
+    PublishArgs a;
+    a.src[0] = u0; a.dst[0] = d_u0; a.words[0] = (size_t)B * 4;
+    a.src[1] = X; a.dst[1] = d_traj; a.words[1] = (size_t)B * (N + 1) * 15;
+    a.src[2] = U; a.dst[2] = d_ctrl; a.words[2] = (size_t)B * N * 4;
+    a.src[3] = diag; a.dst[3] = d_diag; a.words[3] = (size_t)B * 6;
+    a.src[4] = status; a.dst[4] = d_status; a.words[4] = (size_t)B;
+    if (!d_u0 && !d_traj && !d_ctrl && !d_diag && !d_status) return hipSuccess;
+    // the trajectory (B (N+1) 15 words) sets the grid: ~4 words per thread
+    const size_t big = a.words[1];
+    const unsigned gx = (unsigned)std::min<size_t>(std::max<size_t>((big + 1023) / 1024, 1), 4096);
+    hipLaunchKernelGGL(k_publish, dim3(gx, 5), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
 hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, int32_t* lazy,
                            hipStream_t s) {
     hipLaunchKernelGGL(k_qp_order, dim3(1), dim3(1024), 0, s, B, C.K, iters, order, lazy);

@@ -88,6 +88,9 @@ hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double
                      hipStream_t s);
 // QP grid dispatch order: kites by the previous step's iteration count, most
 // first; also empties the lazy state-bound list (lazy[0] = 0, B + 1 entries)
+hipError_t launch_publish(int B, int N, const double* u0, const double* X, const double* U, const double* diag,
+                          const int32_t* status, double* d_u0, double* d_traj, double* d_ctrl, double* d_diag,
+                          int32_t* d_status, hipStream_t s);
 hipError_t launch_qp_order(const RtiConst& C, int B, const int32_t* iters, int32_t* order, int32_t* lazy,
                            hipStream_t s);
 hipError_t launch_dynamics(const ModelConst& P, int count, const double* x, const double* u, double* f,
