@@ -60,6 +60,10 @@ def parse(argv=None):
                          "up to VMAX m/s (kite_nmpc_set_wind; a build extension, the reference model has no "
                          "wind); 0 = no wind, the reference model.  The synthetic ~4.5 m/s kites stay in their "
                          "envelope over a long closed loop up to ~0.5 m/s (DESIGN 2.1)")
+    ap.add_argument("--meas-noise", type=float, default=0.0, metavar="S",
+                    help="disturbed plant: seeded Gaussian noise on every measured state (body velocity and rates "
+                         "0.05 S, position 0.01 S, attitude ~0.01 S rad; openkite_amd/fleet.py MeasurementNoise), "
+                         "so the controller's model no longer predicts the plant exactly; 0 = the nominal loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--latency-steps", type=int, default=1000,
@@ -217,6 +221,8 @@ def run_config_tag(args):
                fp32_sens=bool(args.fp32_sens), ekf=bool(args.ekf), qp_kernel=args.qp_kernel)
     if args.wind_sweep > 0.0:
         tag["wind_sweep"] = args.wind_sweep
+    if args.meas_noise > 0.0:
+        tag["meas_noise"] = args.meas_noise
     return tag
 
 
@@ -331,7 +337,7 @@ def main():
     import torch.distributed as dist
     import openkite_amd as ok
     from openkite_amd import flops
-    from openkite_amd.fleet import FleetLoop, GpuStepper
+    from openkite_amd.fleet import FleetLoop, GpuStepper, MeasurementNoise
     from openkite_amd.shard import Publisher, max_over_ranks, shard
 
     torch.cuda.set_device(local)
@@ -358,8 +364,9 @@ def main():
     if wind is not None:
         ctx.set_wind(wind)
     pub = Publisher(B, dev, world) if distributed and not args.no_allgather else None
+    noise = MeasurementNoise(args.meas_noise, dev, 91_000_000 + rank) if args.meas_noise > 0.0 else None
     loop = FleetLoop(GpuStepper(ctx), torch.from_numpy(x0_host).to(dev), N, cfg.dt, ekf=args.ekf,
-                     covariances=ok.ekf_default_covariances() if args.ekf else None, publisher=pub)
+                     covariances=ok.ekf_default_covariances() if args.ekf else None, publisher=pub, noise=noise)
 
     for _ in range(args.warmup):
         loop.step()
@@ -393,10 +400,19 @@ def main():
         ric = ok.resolve_qp_kernel(args.qp_kernel, N) == 3
         fl = flops.rti_ric(N, args.substeps, mean_it) if ric else flops.rti(N, args.substeps, mean_it)
         kernels = ["prologue", "rk4_sens", "condense", "qp"]
-        avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels}
+        avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels + ["qp_main"]}
         dom = max(kernels, key=lambda k: avg_ms[k])
         dom_flops = fl.get(dom, 0.0) * B
-        achieved = dom_flops / (avg_ms[dom] * 1e-3) / 1e12 if avg_ms[dom] > 0 else 0.0
+        # the QP phase also holds the expansion and the lazy-row launch: its
+        # roofline kernel (k_qp_tiled / k_qp_lds / k_qp / k_qp_ric) is timed
+        # alone by the context's sixth event (kite_nmpc_timing_read)
+        dom_ms = avg_ms["qp_main"] if dom == "qp" else avg_ms[dom]
+        achieved = dom_flops / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else 0.0
+        alt = {}
+        if dom == "qp" and not ric:
+            qm = flops.qp_models(N, mean_it)
+            alt = {f"frac_{k}_count": round(qm[k] * B / (dom_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 5)
+                   for k in ("dense", "survey")}
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12
         qk = ok.resolve_qp_kernel(args.qp_kernel, N)
         traffic, tsrc = pmc_traffic(dominant_kernel_names(dom, qk), run_config_tag(args))
@@ -406,11 +422,16 @@ def main():
         # dependency latency at one wave per SIMD, which is what `bound` says
         roofline = dict(bound="fp64 issue/latency (1 wave/SIMD)", achieved=round(achieved, 4),
                         peak=PEAK_FP64_TFLOPS, unit="TFLOP/s",
-                        frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic, kernel=dom,
+                        frac=round(achieved / PEAK_FP64_TFLOPS, 5), traffic=traffic,
+                        kernel=dominant_kernel_names(dom, ok.resolve_qp_kernel(args.qp_kernel, N))[0],
+                        launch_ms=round(dom_ms, 5), flops_per_launch=dom_flops, **alt,
                         note="fp64 compute roof (dense fp64 MFMA = vector peak on gfx950); the kernel is "
                              "latency-bound (dependent VALU/MFMA/LDS chains at 1 wave/SIMD); achieved = "
-                             "algorithmic flops per launch (openkite_amd/flops.py) / mean launch time (HIP "
-                             f"events on the step stream); traffic = HBM bytes per launch from {tsrc}")
+                             "flops_per_launch (openkite_amd/flops.py, causal count: structurally zero "
+                             "blocks of the condensed C are not work) / launch_ms (HIP events around that "
+                             "kernel alone on the step stream); frac_dense_count / frac_survey_count: the same "
+                             "time priced with dense C and with SURVEY 8(d)'s F_qp; traffic = HBM bytes per "
+                             f"launch from {tsrc}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, x0_host, args.cpu_seconds, wind)
@@ -420,9 +441,10 @@ def main():
         workload = (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
                     + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
                     + (" + fused EKF (BASELINE configs[4])" if args.ekf else
-                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens and wind is None else "")
+                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens and wind is None and noise is None else "")
                     + (f", wind-field sweep |W_h| <= {args.wind_sweep} m/s per instance (build extension)"
-                       if wind is not None else ""))
+                       if wind is not None else "")
+                    + (f", disturbed plant: measurement noise S = {args.meas_noise}" if noise is not None else ""))
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -440,11 +462,13 @@ def main():
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
                        "allgather": pub is not None, "wind_sweep_mps": args.wind_sweep,
+                       "meas_noise": args.meas_noise,
                        "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gpu_latency_batch1": lat1,
-            "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items()},
+            "kernel_ms_per_step": {k: round(v, 4) for k, v in avg_ms.items() if k != "qp_main"},
+            "qp_main_kernel_ms_per_step": round(avg_ms["qp_main"], 4),
             "interval_integrations_per_s": round(world * B * N / (avg_ms["rk4_sens"] * 1e-3), 1)
             if avg_ms["rk4_sens"] > 0 else None,
             "rti_tflops_all_kernels": round(rti_flops, 4),

@@ -35,12 +35,15 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 5   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+#define KITE_NMPC_API_VERSION 6   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
                                       qp_kernel 3 (multiple-shooting QP, Riccati IPM);
                                    3: kite_nmpc_config gained path_harmonics, path_fourier
                                       (arbitrary closed paths); delay_steps default 16;
                                    4: kite_nmpc_state_bound_stats (no config change);
-                                   5: kite_nmpc_set_wind (no config change) */
+                                   5: kite_nmpc_set_wind (no config change);
+                                      qp_soft_weight must exceed 40 (was 20);
+                                   6: kernel_times / timing_read report a sixth
+                                      entry, the main QP kernel alone */
 #define KITE_PATH_MAX_HARMONICS 8 /* Fourier path: harmonics per axis              */
 
 /* ---- error codes ------------------------------------------------------ */
@@ -135,7 +138,9 @@ typedef struct kite_nmpc_config {
     int32_t reserved;
     double qp_soft_weight; /* qp_kernel 3: exact-L1 weight of the state bounds in the reference's
                               scaled units (1e3); the QP stays feasible when the linearised
-                              dynamics cannot meet the box over the horizon                   */
+                              dynamics cannot meet the box over the horizon.  Must exceed
+                              40 = 2 z0 (the IPM's start multiplier, so every soft row starts
+                              dual feasible): smaller values give KITE_EINVAL (since API 5)    */
     double qp_lm;          /* qp_kernel 3: Levenberg-Marquardt term lm/2 ||step||^2 on every QP
                               variable, scaled units (10); leaves the RTI fixed point unchanged */
     /* Arbitrary closed path (KiteNMPF(kite, path), kiteNMPF.h:14, takes any
@@ -309,12 +314,16 @@ int kite_nmpc_ekf_step_device(kite_nmpc_ctx* ctx, int32_t count, double dt, doub
                               const double* d_W169, const double* d_V49);
 
 /* Per-kernel device time [ms] of the last step (cfg.timing = 1):
- * [prologue, rk4_sens, condense, qp, total].  n = entries available (5).    */
+ * [prologue, rk4_sens, condense, qp, total, qp_main]; qp is the whole QP
+ * phase (solve, expansion, lazy state rows), qp_main the main QP kernel
+ * alone (k_qp_tiled / k_qp_lds / k_qp / k_qp_ric: the roofline's kernel).
+ * Returns the entries written, min(n, 6).                                   */
 int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n);
 /* Time every kernel of the next max_steps steps with a ring of HIP events
  * (no host synchronisation between steps); timing_read waits for the last
  * recorded step and returns the number of steps recorded, with per-kernel
- * SUMS [ms] in sums_ms: [prologue, rk4_sens, condense, qp, total].        */
+ * SUMS [ms] in the first min(n, 6) entries of sums_ms:
+ * [prologue, rk4_sens, condense, qp, total, qp_main] (as kernel_times).   */
 int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps);
 int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n);
 /* QP statistics of the last step: final residual and interior-point

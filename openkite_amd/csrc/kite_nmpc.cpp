@@ -24,6 +24,12 @@
 using kite::ModelConst;
 using kite::RtiConst;
 
+// HIP events per timed step: before the prologue, after the prologue, after
+// rk4_sens, after condense + qp_order, after the QP phase (expansion and lazy
+// rows included), and [5] after the main QP kernel alone (k_qp_tiled /
+// k_qp_lds / k_qp / k_qp_ric) -- the roofline's kernel, between [3] and [5]
+constexpr int KITE_NEV = 6;
+
 struct kite_nmpc_ctx {
     kite_params params;
     kite_nmpc_config cfg;
@@ -59,9 +65,10 @@ struct kite_nmpc_ctx {
     // scratch for the model-level entry points
     double* scratch = nullptr;
     size_t scratch_bytes = 0;
-    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[KITE_NEV] = {};
     bool timed_step = false;
-    // event ring for timing a whole run without host syncs (kite_nmpc_timing_start)
+    // event ring for timing a whole run without host syncs (kite_nmpc_timing_start),
+    // KITE_NEV events per step
     std::vector<hipEvent_t> ring;
     int ring_cap = 0, ring_used = 0;
 };
@@ -208,10 +215,10 @@ int validate_config(const kite_nmpc_config& c) {
     if (c.qp_kernel < 0 || c.qp_kernel > 3) return KITE_EINVAL;
     // the multiple-shooting QP's soft-row weight and LM term (the condensed
     // kernels 1 / 2 ignore both): soft_w > 2 z0 keeps the start point of
-    // every soft row dual feasible (z2 = soft_w - z0 > z0, RIC_Z0 = 20)
+    // every soft row dual feasible (z2 = soft_w - z0 > z0, kite::RIC_Z0)
     const int qk = c.qp_kernel ? c.qp_kernel : (c.N == 20 ? 2 : 3);
     if (qk == 3) {
-        if (!(c.qp_soft_weight > 2.0 * 20.0) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;
+        if (!(c.qp_soft_weight > kite::RIC_SOFT_WEIGHT_MIN) || !std::isfinite(c.qp_soft_weight)) return KITE_EINVAL;
         if (!(c.qp_lm >= 0.0) || !std::isfinite(c.qp_lm)) return KITE_EINVAL;
     }
     if (c.sens_fp32 < 0 || c.sens_fp32 > 1) return KITE_EINVAL;
@@ -267,7 +274,7 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     const int B = ctx->B;
     // events: the last-step set (cfg.timing) or the next slot of the ring
     hipEvent_t* ev = nullptr;
-    if (ctx->ring_used < ctx->ring_cap) ev = &ctx->ring[(size_t)ctx->ring_used++ * 5];
+    if (ctx->ring_used < ctx->ring_cap) ev = &ctx->ring[(size_t)ctx->ring_used++ * KITE_NEV];
     else if (ctx->cfg.timing) ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
@@ -301,17 +308,17 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
         const auto* Rd = reinterpret_cast<const kite::RicConst*>(static_cast<const unsigned char*>(ctx->dconst) + roff);
         HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, Cd, Rd, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0,
                                     ctx->diag, ctx->status, ctx->kkt, ctx->iters, ctx->iters + B, ctx->order,
-                                    ctx->Hs, s));
+                                    ctx->Hs, s, ev ? ev[5] : nullptr));
     }
     else if (ctx->tiled)
         HIP_TRY(kite::launch_qp_tiled(ctx->mc, ctx->rc, B, ctx->Htl, ctx->Hab, ctx->Hbb, ctx->hs, ctx->Cr, ctx->cl,
                                       ctx->cu, ctx->hmax, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag,
                                       ctx->status, ctx->kkt, ctx->iters, ctx->order, ctx->order + B, ctx->wstep,
-                                      s));
+                                      s, ev ? ev[5] : nullptr));
     else
         HIP_TRY(kite::launch_qp(ctx->mc, ctx->rc, B, ctx->Hs, ctx->hs, ctx->Cr, ctx->cl, ctx->cu, ctx->hmax, ctx->AB,
                                 ctx->DEF, ctx->X, ctx->U, ctx->u0, ctx->diag, ctx->status, ctx->kkt, ctx->iters,
-                                ctx->order, ctx->order + B, s));
+                                ctx->order, ctx->order + B, s, ev ? ev[5] : nullptr));
     if (ev) HIP_TRY(hipEventRecord(ev[4], s));
     ctx->timed_step = (ev == ctx->ev);
     ctx->warm = true;
@@ -556,6 +563,7 @@ int kite_nmpc_reset(kite_nmpc_ctx* ctx) {
 
 int kite_nmpc_set_wind(kite_nmpc_ctx* ctx, const double* wind) {
     if (!ctx) return KITE_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));      // the wind buffer lives on the context's device
     bool any = false;
     if (wind) {
         for (size_t e = 0; e < (size_t)ctx->B * 3; ++e) {
@@ -943,10 +951,11 @@ int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n) {
     if (!ctx->timed_step) return KITE_ESTATE;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipEventSynchronize(ctx->ev[4]));
-    float v[5];
+    float v[6];
     for (int i = 0; i < 4; ++i) HIP_TRY(hipEventElapsedTime(&v[i], ctx->ev[i], ctx->ev[i + 1]));
     HIP_TRY(hipEventElapsedTime(&v[4], ctx->ev[0], ctx->ev[4]));
-    const int m = n < 5 ? n : 5;
+    HIP_TRY(hipEventElapsedTime(&v[5], ctx->ev[3], ctx->ev[5]));
+    const int m = n < 6 ? n : 6;
     for (int i = 0; i < m; ++i) ms[i] = v[i];
     return m;
 }
@@ -954,7 +963,7 @@ int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n) {
 int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
     if (!ctx || max_steps < 0) return KITE_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
-    const size_t need = (size_t)max_steps * 5;
+    const size_t need = (size_t)max_steps * KITE_NEV;
     while (ctx->ring.size() < need) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
@@ -970,11 +979,11 @@ int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
 int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n) {
     if (!ctx || !sums_ms || n < 1) return KITE_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
-    double acc[5] = {0, 0, 0, 0, 0};
+    double acc[6] = {0, 0, 0, 0, 0, 0};
     const int used = ctx->ring_used;
-    if (used > 0) HIP_TRY(hipEventSynchronize(ctx->ring[(size_t)used * 5 - 1]));
+    if (used > 0) HIP_TRY(hipEventSynchronize(ctx->ring[(size_t)(used - 1) * KITE_NEV + 4]));
     for (int i = 0; i < used; ++i) {
-        hipEvent_t* ev = &ctx->ring[(size_t)i * 5];
+        hipEvent_t* ev = &ctx->ring[(size_t)i * KITE_NEV];
         float v;
         for (int k = 0; k < 4; ++k) {
             HIP_TRY(hipEventElapsedTime(&v, ev[k], ev[k + 1]));
@@ -982,8 +991,10 @@ int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n) {
         }
         HIP_TRY(hipEventElapsedTime(&v, ev[0], ev[4]));
         acc[4] += v;
+        HIP_TRY(hipEventElapsedTime(&v, ev[3], ev[5]));
+        acc[5] += v;
     }
-    const int m = n < 5 ? n : 5;
+    const int m = n < 6 ? n : 6;
     for (int i = 0; i < m; ++i) sums_ms[i] = acc[i];
     ctx->ring_cap = 0;
     ctx->ring_used = 0;

@@ -1965,16 +1965,18 @@ hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
                      int32_t* status, double* kkt, int32_t* iters, const int32_t* order, int32_t* lazy,
-                     hipStream_t s) {
+                     hipStream_t s, hipEvent_t after_main) {
     const int G = B < QP_LAZY_GRID ? B : QP_LAZY_GRID;
     if (C.n <= 82) {
         hipLaunchKernelGGL((k_qp<82>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
                            U, u0, diag, status, kkt, iters, order, lazy);
+        if (after_main) { const hipError_t er = hipEventRecord(after_main, s); if (er != hipSuccess) return er; }
         hipLaunchKernelGGL((k_qp_lazy<82>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF, X,
                            U, u0, diag, status, kkt, iters, order, lazy);
     } else if (C.n <= 162) {
         hipLaunchKernelGGL((k_qp<162>), dim3(B), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
                            X, U, u0, diag, status, kkt, iters, order, lazy);
+        if (after_main) { const hipError_t er = hipEventRecord(after_main, s); if (er != hipSuccess) return er; }
         hipLaunchKernelGGL((k_qp_lazy<162>), dim3(G), dim3(64), 0, s, P, C, B, Hs, hs, Cr, cl, cu, hmax, AB, DEF,
                            X, U, u0, diag, status, kkt, iters, order, lazy);
     } else {

@@ -38,6 +38,13 @@ struct RtiConst {
     double pF[3][KITE_PATH_NC];
 };
 
+// Start multiplier z0 of the multiple-shooting IPM (qp_ric.inc; the oracle's
+// MS_Z0 holds the same value).  A soft state row starts dual feasible only if
+// its weight exceeds 2 z0 (z2 = soft_w - z0 > z0): kite_nmpc_create /
+// set_bounds refuse qp_soft_weight <= RIC_SOFT_WEIGHT_MIN for qp_kernel 3.
+constexpr double RIC_Z0 = 20.0;
+constexpr double RIC_SOFT_WEIGHT_MIN = 2.0 * RIC_Z0;
+
 // Multiple-shooting QP + Riccati interior point (qp_ric.inc, oracle qp_form 1):
 // constants precomputed on the host from kite_nmpc_config.
 struct RicConst {
@@ -63,7 +70,7 @@ size_t qp_ric_ws_doubles(const RtiConst& C);
 hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, const RtiConst* Cd, const RicConst* Rd, int B,
                          const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
                          int32_t* status, double* kkt, int32_t* iters, int32_t* iters_acc, const int32_t* order,
-                         double* ws, hipStream_t s);
+                         double* ws, hipStream_t s, hipEvent_t after_main = nullptr);
 
 // wind: per-kite constant world-frame wind (B x 3, m/s) or nullptr (the
 // reference model, no wind; kite_model.hpp kite_rhs<T, WIND>)
@@ -80,12 +87,13 @@ hipError_t launch_qp_tiled(const ModelConst& P, const RtiConst& C, int B, const 
                            const double* Hbb, const double* hs, const double* Cr, const double* cl,
                            const double* cu, const double* hmax, const double* AB, const double* DEF, double* X,
                            double* U, double* u0, double* diag, int32_t* status, double* kkt, int32_t* iters,
-                           const int32_t* order, int32_t* lazy, double* wstep, hipStream_t s);
+                           const int32_t* order, int32_t* lazy, double* wstep, hipStream_t s,
+                           hipEvent_t after_main = nullptr);
 hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double* Hs, const double* hs,
                      const double* Cr, const double* cl, const double* cu, const double* hmax,
                      const double* AB, const double* DEF, double* X, double* U, double* u0, double* diag,
                      int32_t* status, double* kkt, int32_t* iters, const int32_t* order, int32_t* lazy,
-                     hipStream_t s);
+                     hipStream_t s, hipEvent_t after_main = nullptr);
 // QP grid dispatch order: kites by the previous step's iteration count, most
 // first; also empties the lazy state-bound list (lazy[0] = 0, B + 1 entries)
 hipError_t launch_publish(int B, int N, const double* u0, const double* X, const double* U, const double* diag,

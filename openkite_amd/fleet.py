@@ -13,7 +13,9 @@ One step of a fleet of kites on one rank:
          (shard.Publisher: one all-gather, RCCL over xGMI / gloo on CPU).
   plant  closed loop on synthetic data: the next measured state is the plan's
          prediction at t0 + dt (trajectory node 1), and its position +
-         attitude are the next EKF measurement.
+         attitude are the next EKF measurement.  With ``noise`` (a
+         ``MeasurementNoise``) that state is disturbed before it is measured:
+         the controller's model no longer predicts the plant exactly.
 
 The stepper does the arithmetic; ``GpuStepper`` drives libkite_nmpc.so on
 device tensors.  Tests plug a CPU oracle stepper into the same loop to check
@@ -43,15 +45,42 @@ class GpuStepper:
                                  z.data_ptr() if z is not None else 0, W.data_ptr(), V.data_ptr())
 
 
+class MeasurementNoise:
+    """Seeded Gaussian disturbance of the measured kite state (bench.py
+    --meas-noise): per step and kite, body velocity += 0.05 S, body rates +=
+    0.05 S, position += 0.01 S (N(0, 1) draws, SI units), attitude rotated by
+    a random small angle of about 0.01 S rad (quaternion renormalised);
+    theta / thetadot are the controller's own states and stay untouched.  The
+    draws come from a device generator seeded per rank, so a run is
+    reproducible and the noise costs two small kernels per step."""
+
+    SCALE = (0.05, 0.05, 0.01, 0.005)
+
+    def __init__(self, sigma: float, device, seed: int):
+        self.sigma = float(sigma)
+        self.gen = torch.Generator(device=device)
+        self.gen.manual_seed(int(seed))
+
+    def apply(self, x: torch.Tensor) -> None:
+        B = x.shape[0]
+        n = torch.randn((B, 13), generator=self.gen, dtype=x.dtype, device=x.device)
+        sv, sw, sr, sq = (self.sigma * c for c in self.SCALE)
+        x[:, 0:3] += sv * n[:, 0:3]
+        x[:, 3:6] += sw * n[:, 3:6]
+        x[:, 6:9] += sr * n[:, 6:9]
+        q = x[:, 9:13] + sq * n[:, 9:13]
+        x[:, 9:13] = q / q.norm(dim=1, keepdim=True)
+
+
 class FleetLoop:
     """Closed-loop state of one rank's shard and its per-step sequence."""
 
     def __init__(self, stepper, x0: torch.Tensor, N: int, dt: float, ekf: bool = False, ekf_substeps: int = 5,
-                 covariances: Optional[tuple] = None, publisher=None):
+                 covariances: Optional[tuple] = None, publisher=None, noise: Optional[MeasurementNoise] = None):
         B = x0.shape[0]
         dev = x0.device
         f64 = dict(dtype=torch.float64, device=dev)
-        self.stepper, self.N, self.dt, self.pub = stepper, N, dt, publisher
+        self.stepper, self.N, self.dt, self.pub, self.noise = stepper, N, dt, publisher, noise
         self.x0 = x0.clone()
         self.u0 = torch.zeros((B, 4), **f64)
         self.traj = torch.zeros((B, N + 1, 15), **f64)
@@ -82,8 +111,10 @@ class FleetLoop:
                                  self.W, self.V)
             self.x0[:, :13].copy_(self.xe)
         self.stepper.rti(self.x0, self.u0, self.traj, self.diag, self.status)
-        if self.ekf:
-            self.z.copy_(self.traj[:, 1, 6:13])
         if self.pub is not None:
             self.gathered = self.pub.publish(self.u0, self.diag)
         self.x0.copy_(self.traj[:, 1, :])
+        if self.noise is not None:
+            self.noise.apply(self.x0)
+        if self.ekf:
+            self.z.copy_(self.x0[:, 6:13])

@@ -13,11 +13,21 @@ Per instance:
              kernel recomputes it on each of the 16 lanes: that redundancy is
              an implementation cost, not algorithmic work).
   condense : G-column propagation  sum_k (3k+1) * 2*NK^2  (+ defects)
-             + H_ext = W^T W on the (4N+3) x (n+1) residual Jacobian,
-               symmetric half: rows * (n+1)(n+2)/2 * 2
-  qp       : per interior-point iteration, n = 4N+2, m = N:
-             H w 2n^2, C w and C^T z 4mn, normal matrix n(n+1)/2 * (2m+1),
-             Cholesky n^3/3, two solves 2 * (2n^2 + 4mn)
+             + H_ext = W^T W, causal: the residual rows of node k (4, the
+               Mayer node 3) reach only the c_k = 4k + 3 columns of the
+               controls of intervals < k, theta0, thetadot0 and the affine
+               column, so node k adds rows_k * c_k (c_k + 1) / 2 * 2
+               (condense_dense: the dense (4N+3) x (n+1) Jacobian,
+               rows * (n+1)(n+2)/2 * 2)
+  qp       : per interior-point iteration, n = 4N+2, m = N vx rows; C is
+             causal: the vx row of node k reaches only the 3k kite controls
+             of intervals < k, nnz(C) = 3N(N+1)/2 (630 of m n = 1640 at N = 20):
+             H w 2n^2, C w and C^T z 4 nnz(C), normal matrix H + C^T Sigma C
+             n(n+1)/2 + sum_k 3k(3k+1) (symmetric half of each row's outer
+             product), Cholesky n^3/3, two solves 2 * (2n^2 + 4 nnz(C)).
+             Two other counts are kept beside it (qp_models): the dense count
+             (C as a dense m x n matrix: 4mn and n(n+1)/2 (2m+1)) and
+             SURVEY.md 8(d)'s F_qp = n^3/3 + 4 n^2 + m n^2 per iteration.
   qp_ric   : the multiple-shooting QP (qp_kernel 3, no condensing), per
              interior-point iteration and stage (nx = 15 states, nu = 4
              controls, the kite block Z = [A | B] is 13 x 16):
@@ -49,23 +59,56 @@ def rk4_sens(N: int, M: int) -> float:
     return N * rk4_sens_per_interval(M)
 
 
+def _propagation(N: int) -> float:
+    return sum((3 * k + 1) * 2 * NK * NK + NK for k in range(N))
+
+
 def condense(N: int) -> float:
+    syrk = sum((4 if k < N else 3) * (4 * k + 3) * (4 * k + 4) for k in range(N + 1))
+    return _propagation(N) + syrk
+
+
+def condense_dense(N: int) -> float:
     n = 4 * N + 2
-    prop = sum((3 * k + 1) * 2 * NK * NK + NK for k in range(N))
     rows = 4 * N + 3
-    syrk = rows * (n + 1) * (n + 2) / 2 * 2
-    return prop + syrk
+    return _propagation(N) + rows * (n + 1) * (n + 2) / 2 * 2
+
+
+def c_nnz(N: int) -> int:
+    """Structural nonzeros of the condensed vx rows C (row k: 3k kite controls)."""
+    return 3 * N * (N + 1) // 2
 
 
 def qp_per_iteration(N: int) -> float:
+    n, c = 4 * N + 2, c_nnz(N)
+    normal = n * (n + 1) / 2 + sum(3 * k * (3 * k + 1) for k in range(1, N + 1))
+    return 2 * n * n + 4 * c + normal + n ** 3 / 3 + 2 * (2 * n * n + 4 * c)
+
+
+def qp_per_iteration_dense(N: int) -> float:
     n, m = 4 * N + 2, N
     return 2 * n * n + 4 * m * n + n * (n + 1) / 2 * (2 * m + 1) + n ** 3 / 3 + 2 * (2 * n * n + 4 * m * n)
 
 
+def qp_per_iteration_survey(N: int) -> float:
+    """F_qp / K = n^3/3 + 4 n^2 + n_c n^2 (n_c = N rows)."""
+    n = 4 * N + 2
+    return n ** 3 / 3 + 4 * n * n + N * n * n
+
+
 def qp(N: int, iterations: float) -> float:
     # the final residual evaluation is one more H w / C w pass
-    n, m = 4 * N + 2, N
-    return iterations * qp_per_iteration(N) + 2 * n * n + 4 * m * n
+    n = 4 * N + 2
+    return iterations * qp_per_iteration(N) + 2 * n * n + 4 * c_nnz(N)
+
+
+def qp_models(N: int, iterations: float) -> dict:
+    """The condensed QP's flops per instance under the three counts: causal
+    (`qp`, what bench.py's roofline uses), dense C, and SURVEY 8(d)'s F_qp."""
+    n = 4 * N + 2
+    return dict(causal=qp(N, iterations),
+                dense=iterations * qp_per_iteration_dense(N) + 2 * n * n + 4 * N * n,
+                survey=iterations * qp_per_iteration_survey(N))
 
 
 def rti(N: int, M: int, mean_qp_iterations: float) -> dict:

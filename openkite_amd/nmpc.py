@@ -338,19 +338,25 @@ class BatchNMPC:
     def set_solution(self, traj, ctrl):
         _check(lib().kite_nmpc_set_solution(self._h, _p(_f64(traj)), _p(_f64(ctrl))), "set_solution")
 
+    TIMING_KEYS = ("prologue", "rk4_sens", "condense", "qp", "total", "qp_main")
+
     def kernel_times(self):
-        ms = np.zeros(5)
-        n = _check(lib().kite_nmpc_kernel_times(self._h, _p(ms), 5), "kernel_times")
-        return dict(zip(["prologue", "rk4_sens", "condense", "qp", "total"], ms[:n]))
+        """Device time [ms] of the last step per phase (config.timing = 1);
+        qp is the QP phase (solve + expansion + lazy rows), qp_main the main
+        QP kernel alone."""
+        ms = np.zeros(6)
+        n = _check(lib().kite_nmpc_kernel_times(self._h, _p(ms), 6), "kernel_times")
+        return dict(zip(self.TIMING_KEYS, ms[:n]))
 
     def timing_start(self, max_steps: int):
         _check(lib().kite_nmpc_timing_start(self._h, int(max_steps)), "timing_start")
 
     def timing_read(self):
-        """Per-kernel SUMS [ms] over the steps recorded since timing_start."""
-        ms = np.zeros(5)
-        n = _check(lib().kite_nmpc_timing_read(self._h, _p(ms), 5), "timing_read")
-        return n, dict(zip(["prologue", "rk4_sens", "condense", "qp", "total"], ms))
+        """Per-phase SUMS [ms] over the steps recorded since timing_start
+        (keys as kernel_times)."""
+        ms = np.zeros(6)
+        n = _check(lib().kite_nmpc_timing_read(self._h, _p(ms), 6), "timing_read")
+        return n, dict(zip(self.TIMING_KEYS, ms))
 
     def qp_stats(self):
         kkt = np.zeros(self.batch); it = np.zeros(self.batch, dtype=np.int32)

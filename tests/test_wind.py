@@ -184,13 +184,20 @@ def test_gpu_rti_under_wind_vs_oracle(kp, Nh):
             assert not np.any(r["status"] & 1) and not np.any(st & 1)
             np.testing.assert_array_equal(r["status"] & ~(2 | 32), st & ~(2 | 32))
             if Nh == 20:
+                np.testing.assert_array_equal(r["status"] & 32, st & 32)
                 assert_cond_rti(r, u0, Xo, Uo, (Nh, step))
             else:
+                # the step safeguard (bit 32: residual >= 1e-6 at the cap) may decide
+                # differently only where the two capped residuals straddle 1e-6
+                # within a decade (as in test_gpu_parity._config5_vs_oracle)
+                kg, ko = g.qp_stats()[0], diag[:, 5]
+                flip = (np.minimum(kg, ko) < 1e-6) & (np.maximum(kg, ko) >= 1e-6) & (np.maximum(kg, ko) < 1e-5)
                 same = (r["status"] & 32) == (st & 32)
-                assert same.mean() >= 0.98
+                assert np.all(same | flip), (step, np.where(~same)[0], kg[~same], ko[~same])
+                assert np.sum(~same) <= max(1, B // 50), np.where(~same)[0]
                 e = np.maximum.reduce([rel_per_kite(r["u0"], u0), rel_per_kite(r["traj"], Xo),
                                        rel_per_kite(r["ctrl"], Uo)])[same]
-                assert_ms_rti(e, g.qp_stats()[0][same], diag[same, 5], (Nh, step))
+                assert_ms_rti(e, kg[same], ko[same], (Nh, step))
             x = Xo[:, 1, :].copy()
     finally:
         g.close()

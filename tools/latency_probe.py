@@ -1,0 +1,59 @@
+"""Single-kite latency decomposition: for a batch-1
+context at N = 20, a warm closed loop of `steps` steps, the wall time of
+kite_nmpc_step (host arrays in and out, synchronous) and of
+kite_nmpc_step_device + stream synchronisation, next to the device time of
+every phase (config.timing = 1: HIP events of the last step).  Tools only.
+  python tools/latency_probe.py [steps] [N] [batch]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import torch  # noqa: E402
+
+import openkite_amd as ok  # noqa: E402
+from test_gpu_parity import x0_batch  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+Nh = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+Bt = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+cfg = ok.default_config(N=Nh, timing=1)
+g = ok.BatchNMPC(ok.load_properties(), cfg, Bt)
+x = x0_batch(Bt)
+wall, ph = [], []
+for i in range(steps + 20):
+    t0 = time.perf_counter()
+    r = g.step(x)
+    t1 = time.perf_counter()
+    x = r["traj"][:, 1, :].copy()
+    if i >= 20:
+        wall.append(t1 - t0)
+        ph.append(g.kernel_times())
+out = dict(batch=Bt, N=Nh, steps=steps, host_step_median_ms=float(np.median(wall) * 1e3),
+           host_step_p90_ms=float(np.percentile(wall, 90) * 1e3),
+           phases_median_ms={k: float(np.median([p[k] for p in ph])) for k in ph[0]})
+# device entry point on torch's stream, synchronised per step (inputs in HBM)
+g.set_stream(torch.cuda.current_stream().cuda_stream)
+d_x = torch.from_numpy(x.copy()).cuda()
+d_u = torch.zeros((Bt, 4), dtype=torch.float64, device="cuda")
+d_t = torch.zeros((Bt, Nh + 1, 15), dtype=torch.float64, device="cuda")
+d_d = torch.zeros((Bt, 6), dtype=torch.float64, device="cuda")
+d_s = torch.zeros((Bt,), dtype=torch.int32, device="cuda")
+wd = []
+for i in range(steps + 20):
+    t0 = time.perf_counter()
+    g.step_device(d_x.data_ptr(), d_u.data_ptr(), d_t.data_ptr(), 0, d_d.data_ptr(), d_s.data_ptr())
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    d_x.copy_(d_t[:, 1, :])
+    if i >= 20:
+        wd.append(t1 - t0)
+out["device_step_median_ms"] = float(np.median(wd) * 1e3)
+out["device_step_p90_ms"] = float(np.percentile(wd, 90) * 1e3)
+g.close()
+print(json.dumps(out), flush=True)
