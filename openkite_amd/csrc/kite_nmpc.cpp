@@ -60,7 +60,8 @@ struct kite_nmpc_ctx {
     double *Htl = nullptr, *Hab = nullptr, *Hbb = nullptr;
     double* wind = nullptr;        // per-kite world-frame wind B x 3 (kite_nmpc_set_wind)
     bool has_wind = false;         // a nonzero wind is set: the WIND kernels run
-    double* wstep = nullptr;       // tiled path: physical QP step per kite (k_qp_tiled -> k_expand20); N = 40:
+    double* wstep = nullptr;       // tiled path, 2 B n: physical QP step per kite (k_qp_tiled -> k_expand20), then
+                                   // the scaled one (-> k_qp_tiled_lazy: round 0 handed over); N = 40:
                                    // round-0 solution of the kites k_qp_lds hands to k_qp_lds_lazy
     // scratch for the model-level entry points
     double* scratch = nullptr;
@@ -496,7 +497,7 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         {&ctx->Cr, ctx->ric ? 1 : B * N * n}, {&ctx->cl, ctx->ric ? 1 : B * N}, {&ctx->cu, ctx->ric ? 1 : B * N},
         {&ctx->hmax, B}, {&ctx->u0, B * 4}, {&ctx->diag, B * 6}, {&ctx->kkt, B},
         {&ctx->Htl, ctx->tiled ? B * ntile * 256 : 1}, {&ctx->Hab, ctx->tiled ? B * na * 2 : 1},
-        {&ctx->Hbb, ctx->tiled ? B * 4 : 1}, {&ctx->wstep, ctx->tiled ? B * n : 1},
+        {&ctx->Hbb, ctx->tiled ? B * 4 : 1}, {&ctx->wstep, ctx->tiled ? 2 * B * n : 1},
     };
     for (const Alloc& a : allocs) {
         if (hipMalloc(a.p, a.count * sizeof(double)) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }

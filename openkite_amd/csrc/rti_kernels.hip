@@ -1404,6 +1404,7 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
     __shared__ double vec[NQ + 2];
     __shared__ double col[NQ];
     __shared__ double dinv[NQ];
+    __shared__ double eq[NQ];          // equilibration E = diag(M)^-1/2 of the current factorization
     __shared__ double sbnd[32], sXc[LAZY_ROWS];
     __shared__ int sel[3 * LAZY_ROWS];
 
@@ -1572,8 +1573,11 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
             __syncthreads();
         }
     };
-    // x <- M^-1 x with x in per-lane slots (2)
+    // x <- M^-1 x = E (E M E)^-1 E x with x in per-lane slots (NS); Lp holds
+    // the factor of E M E
     auto chol_solve = [&](double x[NS]) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { const int i = l + 64 * s; if (i < n) x[s] *= eq[i]; }
         for (int k = 0; k < n; ++k) {
             double xk;
             xk = slot_pivot<NS>(x, k, l) * dinv[k];
@@ -1598,6 +1602,8 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
                 if (i < k) x[s] = fma(-Lp[pk(k, i)], xk, x[s]);
             }
         }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { const int i = l + 64 * s; if (i < n) x[s] *= eq[i]; }
     };
 
     double sgl[NS], sgu[NS], sglo = 0.0, sghi = 0.0;
@@ -1696,6 +1702,26 @@ __device__ __forceinline__ void qp_body(int b, ModelConst /*P*/, RtiConst C, int
                     if (c == rr) mv += sgl[s] + sgu[s];
                     Lp[pk(rr, c)] = mv;
                 }
+            }
+        }
+        __syncthreads();
+        // equilibrate M <- E M E, E = diag(M)^-1/2 (as k_qp_tiled / k_qp_lds):
+        // near convergence the barrier weights spread the diagonal over ~24
+        // decades, and unequilibrated the last factorizations of an ill-
+        // conditioned QP (N = 40: a pivot at 4e-15 of its diagonal) left the
+        // step along the Hessian's near-null directions to rounding
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int i = l + 64 * s;
+            if (i < n) eq[i] = 1.0 / sqrt(piv_fix(Lp[pk(i, i)]));
+        }
+        __syncthreads();
+        for (int rr = 0; rr < n; ++rr) {
+            const double er = eq[rr];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int c = l + 64 * s;
+                if (c <= rr) Lp[pk(rr, c)] *= er * eq[c];
             }
         }
         __syncthreads();

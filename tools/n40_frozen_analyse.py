@@ -20,6 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 from oracle import ffi  # noqa: E402
 from test_gpu_parity import condensed_cfgv, gpu_to_oracle_perm  # noqa: E402
 
@@ -34,7 +35,7 @@ def plan_of(q, Xp, Up, w):
     """Plan (traj, ctrl) of scaled step w at the linearisation point, as the
     oracle's expansion: dx = G D w (G from build_qp), du = D w."""
     dw = q["D"] * w
-    traj = Xp + np.einsum("kin,n->ki", q["G"], dw)
+    traj = Xp + q["g"] + np.einsum("kin,n->ki", q["G"], dw)
     ctrl = Up + dw[:4 * Nh].reshape(Nh, 4)
     return traj, ctrl
 
@@ -52,8 +53,8 @@ def main(d, qks):
         z = np.load(os.path.join(d, f"n40_frozen_qk{qk}.npz"))
         S, B = z["kkt_g"].shape
         print(f"=== qp_kernel {qk}: {S} steps x {B} kites")
-        print(" st  k  e_plan    kkt_g    kkt_o    dH       dh       dC       s_solve  s_data   s_1e15   s_meas   "
-              "kkt_og   it_og")
+        print(" st  k  e_plan    kkt_g    kkt_o    it_g it_o dH       dh       dC       s_solve  s_data   s_1e15   "
+              "s_meas   kkt_og   e_capped")
         worst = None
         for s in range(S):
             for b in range(B):
@@ -81,13 +82,43 @@ def main(d, qks):
                 t2, u2 = plan_of(q, Xp, Up, w2)
                 s15 = max(rel(t1, to), rel(u1, uo)) if k1 < 1e-10 and ko < 1e-10 else np.nan
                 sm = max(rel(t2, to), rel(u2, uo)) if k2 < 1e-10 and ko < 1e-10 else np.nan
-                print(f" {s}  {b:2d} {e_plan:8.1e} {z['kkt_g'][s, b]:8.1e} {z['diag_o'][s, b, 5]:8.1e} {dH:8.1e} "
-                      f"{dh:8.1e} {dC:8.1e} {s_solve:8.1e} {s_data:8.1e} {s15:8.1e} {sm:8.1e} {kg:8.1e}")
+                # the oracle's own RTI step on this kite, its iteration count, and
+                # the same step with the IPM capped at the GPU's iteration count
+                def orc(Kc):
+                    X1, U1 = z["Xin"][s, b][None].copy(), z["Uin"][s, b][None].copy()
+                    its = np.zeros(1, dtype=np.int32)
+                    ffi.rti_step(kp, cv, Nh, M, Kc, z["x"][s, b][None].copy(), X1, U1, warm=int(s > 0), iters=its)
+                    return X1[0], U1[0], int(its[0])
+                _, _, it_o = orc(K)
+                it_g = int(z["it_g"][s, b])
+                Xc, Uc, _ = orc(it_g) if it_g > 0 else (None, None, 0)
+                e_cap = max(rel(z["traj_g"][s, b], Xc), rel(z["ctrl_g"][s, b], Uc)) if it_g > 0 else np.nan
+                print(f" {s}  {b:2d} {e_plan:8.1e} {z['kkt_g'][s, b]:8.1e} {z['diag_o'][s, b, 5]:8.1e} {it_g:4d} "
+                      f"{it_o:4d} {dH:8.1e} {dh:8.1e} {dC:8.1e} {s_solve:8.1e} {s_data:8.1e} {s15:8.1e} {sm:8.1e} "
+                      f"{kg:8.1e} {e_cap:8.1e}")
                 if worst is None or e_plan > worst[0]:
                     worst = (e_plan, s, b, q, Hg, hg, Cg, wo, wg, Xp, Up)
         e_plan, s, b, q, Hg, hg, Cg, wo, wg, Xp, Up = worst
         print(f"--- worst kite: step {s} kite {b}, plan error {e_plan:.2e}")
-        dw = wg - wo
+        # the GPU's scaled step, recovered from its plan (du = D w on the controls,
+        # dtheta0 / dthetadot0 = D w on the last two variables)
+        Dv = q["D"]
+        wgpu = np.concatenate([(z["ctrl_g"][s, b] - Up).reshape(-1), z["traj_g"][s, b][0, 13:15] - Xp[0, 13:15]]) / Dv
+        rd_o = q["H"] @ wo + q["h"]
+        rd_g = q["H"] @ wgpu + q["h"]
+        print(f"  GPU step vs oracle step: |w_gpu - w_oo|_inf {np.abs(wgpu - wo).max():.2e}; max|H| "
+              f"{np.abs(q['H']).max():.2e} (freeze test scales the dual residual by 1/(1 + max|H|))")
+        print(f"  cost at w_oo {cost(q['H'], q['h'], wo):.12e}, at w_gpu {cost(q['H'], q['h'], wgpu):.12e}")
+        # a third fp64 implementation of the same IPM, differing only in its
+        # rounding (numpy replica of qp_ipm, LAPACK Cholesky, same z0 / freeze)
+        from warm_ipm_probe import ipm
+        wn, _, _, itn, rn = ipm(q, K, z_init=20.0)
+        print(f"  numpy/LAPACK replica: {itn} iterations, residual {rn:.1e}, |w_np - w_oo|_inf "
+              f"{np.abs(wn - wo).max():.2e}, |w_np - w_gpu|_inf {np.abs(wn - wgpu).max():.2e}")
+        dw = wgpu - wo
+        print(f"  Rayleigh quotient of w_gpu - w_oo: {dw @ q['H'] @ dw / (dw @ dw):.2e} (max|H| "
+              f"{np.abs(q['H']).max():.2e}); of w_np - w_oo: "
+              f"{(wn - wo) @ q['H'] @ (wn - wo) / max((wn - wo) @ (wn - wo), 1e-300):.2e}")
         print(f"  |w_og - w_oo|_inf {np.abs(dw).max():.2e}; cost(H_o) at w_oo {cost(q['H'], q['h'], wo):.12e}, "
               f"at w_og {cost(q['H'], q['h'], wg):.12e}")
         # active set at the oracle solution and the reduced Hessian on its null space
