@@ -72,6 +72,18 @@ struct kite_nmpc_ctx {
     // KITE_NEV events per step
     std::vector<hipEvent_t> ring;
     int ring_cap = 0, ring_used = 0;
+    // kite_nmpc_step's launch sequence (x0 in, every kernel of the step, the
+    // outputs out) captured once per warm / cold start into a HIP graph, with
+    // pinned host staging: one graph launch and one synchronisation per step
+    // instead of ~10 launches and 6 pageable copies (the ROS node's batch-1
+    // latency).  Captured kernels take the context constants by value, so the
+    // setters that change them bump graph_gen and the graphs are re-captured.
+    hipGraphExec_t gexec[2] = {nullptr, nullptr};  // [warm]
+    unsigned graph_gen = 0, gexec_gen[2] = {0, 0};
+    bool graph_off = false;                         // KITE_NMPC_NO_GRAPH=1 (A/B runs)
+    double* h_in = nullptr;                         // pinned: B x 15
+    unsigned char* h_out = nullptr;                 // pinned: u0 | traj | ctrl | diag | status
+    unsigned char* d_out = nullptr;                 // device staging of the same layout
 };
 
 namespace {
@@ -264,7 +276,30 @@ void free_ctx(kite_nmpc_ctx* ctx) {
     for (auto& e : ctx->ev) if (e) { (void)hipEventDestroy(e); e = nullptr; }
     for (auto& e : ctx->ring) if (e) (void)hipEventDestroy(e);
     ctx->ring.clear();
+    for (auto& g : ctx->gexec) if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    if (ctx->h_in) { (void)hipHostFree(ctx->h_in); ctx->h_in = nullptr; }
+    if (ctx->h_out) { (void)hipHostFree(ctx->h_out); ctx->h_out = nullptr; }
+    if (ctx->d_out) { (void)hipFree(ctx->d_out); ctx->d_out = nullptr; }
     if (ctx->own_stream) { (void)hipStreamDestroy(ctx->own_stream); ctx->own_stream = nullptr; }
+}
+
+// The multiple-shooting QP reads (rc, ricc) from device memory (ctx->dconst):
+// re-uploaded on `s` when the host copy changed since the last upload.
+int upload_dconst(kite_nmpc_ctx* ctx, hipStream_t s) {
+    constexpr size_t roff = (sizeof(kite::RtiConst) + 255) / 256 * 256;
+    static_assert(roff + sizeof(kite::RicConst) <= 4096, "dconst holds both constant blocks");
+    unsigned char blob[roff + sizeof(kite::RicConst)] = {};
+    std::memcpy(blob, &ctx->rc, sizeof(kite::RtiConst));
+    std::memcpy(blob + roff, &ctx->ricc, sizeof(kite::RicConst));
+    if (ctx->dconst_host.size() != sizeof(blob) || std::memcmp(ctx->dconst_host.data(), blob, sizeof(blob))) {
+        // the host mirror is what the device holds: set only once the copy
+        // is enqueued (a failed copy leaves it empty, so the next step retries)
+        ctx->dconst_host.clear();
+        ctx->dconst_stage.assign(blob, blob + sizeof(blob));
+        HIP_TRY(hipMemcpyAsync(ctx->dconst, ctx->dconst_stage.data(), sizeof(blob), hipMemcpyHostToDevice, s));
+        ctx->dconst_host.swap(ctx->dconst_stage);
+    }
+    return KITE_OK;
 }
 
 // Runs the RTI kernels on ctx->stream.  x0: B x 15 measured states in device
@@ -293,18 +328,7 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
     if (ctx->ric) {
         constexpr size_t roff = (sizeof(kite::RtiConst) + 255) / 256 * 256;
-        static_assert(roff + sizeof(kite::RicConst) <= 4096, "dconst holds both constant blocks");
-        unsigned char blob[roff + sizeof(kite::RicConst)] = {};
-        std::memcpy(blob, &ctx->rc, sizeof(kite::RtiConst));
-        std::memcpy(blob + roff, &ctx->ricc, sizeof(kite::RicConst));
-        if (ctx->dconst_host.size() != sizeof(blob) || std::memcmp(ctx->dconst_host.data(), blob, sizeof(blob))) {
-            // the host mirror is what the device holds: set only once the copy
-            // is enqueued (a failed copy leaves it empty, so the next step retries)
-            ctx->dconst_host.clear();
-            ctx->dconst_stage.assign(blob, blob + sizeof(blob));
-            HIP_TRY(hipMemcpyAsync(ctx->dconst, ctx->dconst_stage.data(), sizeof(blob), hipMemcpyHostToDevice, s));
-            ctx->dconst_host.swap(ctx->dconst_stage);
-        }
+        { const int urc = upload_dconst(ctx, s); if (urc) return urc; }
         const auto* Cd = reinterpret_cast<const kite::RtiConst*>(ctx->dconst);
         const auto* Rd = reinterpret_cast<const kite::RicConst*>(static_cast<const unsigned char*>(ctx->dconst) + roff);
         HIP_TRY(kite::launch_qp_ric(ctx->rc, ctx->ricc, Cd, Rd, B, ctx->AB, ctx->DEF, ctx->X, ctx->U, ctx->u0,
@@ -323,6 +347,71 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     if (ev) HIP_TRY(hipEventRecord(ev[4], s));
     ctx->timed_step = (ev == ctx->ev);
     ctx->warm = true;
+    return KITE_OK;
+}
+
+// ---- the captured host step (kite_nmpc_step) -------------------------------
+// output staging layout in bytes: u0 B x 4 | traj B x (N+1) x 15 | ctrl B x N x 4 |
+// diag B x 6 (doubles) | status B (int32)
+struct OutLayout {
+    size_t u0, traj, ctrl, diag, status, total;
+};
+OutLayout out_layout(size_t B, size_t N) {
+    OutLayout o;
+    o.u0 = 0;
+    o.traj = o.u0 + B * 4 * sizeof(double);
+    o.ctrl = o.traj + B * (N + 1) * 15 * sizeof(double);
+    o.diag = o.ctrl + B * N * 4 * sizeof(double);
+    o.status = o.diag + B * 6 * sizeof(double);
+    o.total = o.status + B * sizeof(int32_t);
+    return o;
+}
+
+int ensure_staging(kite_nmpc_ctx* ctx) {
+    if (ctx->h_in && ctx->h_out && ctx->d_out) return KITE_OK;
+    const OutLayout o = out_layout(ctx->B, ctx->cfg.N);
+    if (!ctx->h_in) HIP_TRY(hipHostMalloc((void**)&ctx->h_in, (size_t)ctx->B * 15 * sizeof(double)));
+    if (!ctx->h_out) HIP_TRY(hipHostMalloc((void**)&ctx->h_out, o.total));
+    if (!ctx->d_out) HIP_TRY(hipMalloc((void**)&ctx->d_out, o.total));
+    return KITE_OK;
+}
+
+// Captures x0 in (pinned -> device), run_step and the outputs out (one fused
+// publish kernel into device staging, one copy to pinned memory) for the given
+// warm flag.  No events are recorded (the caller checks that no timing is on).
+int capture_step(kite_nmpc_ctx* ctx, int warm) {
+    const size_t B = ctx->B, N = ctx->cfg.N;
+    const OutLayout o = out_layout(B, N);
+    hipStream_t cs = ctx->own_stream;
+    hipStream_t saved_stream = ctx->stream;
+    const bool saved_warm = ctx->warm;
+    ctx->stream = cs;
+    ctx->warm = warm != 0;
+    HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+    int rc = KITE_OK;
+    hipError_t e = hipMemcpyAsync(ctx->x0, ctx->h_in, B * 15 * sizeof(double), hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) rc = run_step(ctx, ctx->x0);
+    if (e == hipSuccess && rc == KITE_OK)
+        e = kite::launch_publish((int)B, (int)N, ctx->u0, ctx->X, ctx->U, ctx->diag, ctx->status,
+                                 (double*)(ctx->d_out + o.u0), (double*)(ctx->d_out + o.traj),
+                                 (double*)(ctx->d_out + o.ctrl), (double*)(ctx->d_out + o.diag),
+                                 (int32_t*)(ctx->d_out + o.status), cs);
+    if (e == hipSuccess && rc == KITE_OK) e = hipMemcpyAsync(ctx->h_out, ctx->d_out, o.total, hipMemcpyDeviceToHost, cs);
+    hipGraph_t graph = nullptr;
+    const hipError_t ee = hipStreamEndCapture(cs, &graph);
+    ctx->stream = saved_stream;
+    ctx->warm = saved_warm;
+    if (rc != KITE_OK || e != hipSuccess || ee != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc != KITE_OK ? rc : hip_fail(e != hipSuccess ? e : ee);
+    }
+    hipGraphExec_t ex = nullptr;
+    e = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return hip_fail(e);
+    if (ctx->gexec[warm]) (void)hipGraphExecDestroy(ctx->gexec[warm]);
+    ctx->gexec[warm] = ex;
+    ctx->gexec_gen[warm] = ctx->graph_gen;
     return KITE_OK;
 }
 
@@ -516,6 +605,10 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         free_ctx(ctx); delete ctx; return KITE_EHIP;
     }
     ctx->stream = ctx->own_stream;
+    {
+        const char* ng = std::getenv("KITE_NMPC_NO_GRAPH");
+        ctx->graph_off = ng && ng[0] == '1';
+    }
     for (auto& e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
     if (hipDeviceSynchronize() != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
@@ -546,6 +639,7 @@ int kite_nmpc_set_bounds(kite_nmpc_ctx* ctx, const double* lbx15, const double* 
     ctx->cfg = c;
     ctx->rc = make_rti_const(c);
     if (ctx->ric) ctx->ricc = make_ric_const(c);     // the QP's bounds
+    ++ctx->graph_gen;                                // captured kernels hold rc by value
     return KITE_OK;
 }
 
@@ -553,6 +647,7 @@ int kite_nmpc_set_reference_velocity(kite_nmpc_ctx* ctx, double vref) {
     if (!ctx || !std::isfinite(vref)) return KITE_EINVAL;
     ctx->cfg.vref = vref;
     ctx->rc = make_rti_const(ctx->cfg);
+    ++ctx->graph_gen;
     return KITE_OK;
 }
 
@@ -572,6 +667,7 @@ int kite_nmpc_set_wind(kite_nmpc_ctx* ctx, const double* wind) {
             any = any || wind[e] != 0.0;
         }
     }
+    ++ctx->graph_gen;                                    // the wind selects other kernels
     if (!any) { ctx->has_wind = false; return KITE_OK; }   // the reference model
     if (!ctx->wind) HIP_TRY(hipMalloc(&ctx->wind, (size_t)ctx->B * 3 * sizeof(double)));
     // ordered with the steps on the context stream (the host array may be
@@ -621,6 +717,35 @@ int kite_nmpc_step(kite_nmpc_ctx* ctx, const double* x0, double* u0_out, double*
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t B = ctx->B, N = ctx->cfg.N;
     hipStream_t s = ctx->stream;
+    // the captured step: no per-kernel timing requested (cfg.timing, a live
+    // timing_start ring); otherwise the launches below record their events
+    if (!ctx->graph_off && !ctx->cfg.timing && ctx->ring_used >= ctx->ring_cap) {
+        int rc = ensure_staging(ctx);
+        if (rc) return rc;
+        if (ctx->ric) { rc = upload_dconst(ctx, s); if (rc) return rc; }   // outside the graph
+        const int w = ctx->warm ? 1 : 0;
+        if (!ctx->gexec[w] || ctx->gexec_gen[w] != ctx->graph_gen) {
+            rc = capture_step(ctx, w);
+            if (rc) return rc;
+        }
+        std::memcpy(ctx->h_in, x0, B * 15 * sizeof(double));
+        HIP_TRY(hipGraphLaunch(ctx->gexec[w], s));
+        HIP_TRY(hipStreamSynchronize(s));
+        ctx->warm = true;
+        ctx->timed_step = false;
+        const OutLayout o = out_layout(B, N);
+        if (u0_out) std::memcpy(u0_out, ctx->h_out + o.u0, B * 4 * sizeof(double));
+        if (traj_out) std::memcpy(traj_out, ctx->h_out + o.traj, B * (N + 1) * 15 * sizeof(double));
+        if (ctrl_out) std::memcpy(ctrl_out, ctx->h_out + o.ctrl, B * N * 4 * sizeof(double));
+        if (status_out) std::memcpy(status_out, ctx->h_out + o.status, B * sizeof(int32_t));
+        if (diag_out) {
+            static_assert(sizeof(kite_mpc_diagnostic) == 6 * sizeof(double), "diagnostic layout");
+            std::memcpy(diag_out, ctx->h_out + o.diag, B * 6 * sizeof(double));
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            for (size_t b = 0; b < B; ++b) diag_out[b].comp_time_ms = ms;
+        }
+        return KITE_OK;
+    }
     HIP_TRY(hipMemcpyAsync(ctx->x0, x0, B * 15 * sizeof(double), hipMemcpyHostToDevice, s));
     int rc = run_step(ctx, ctx->x0);
     if (rc) return rc;

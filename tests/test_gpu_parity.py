@@ -45,10 +45,12 @@ COND_ENVELOPE = 1e-5  # condensed QP frozen on both sides: a 1e-15 relative pert
 
 def assert_cond_rti(r, u0, Xo, Uo, where):
     """Condensed RTI step vs the oracle, per kite: every kite within the QP's
-    sensitivity envelope COND_ENVELOPE, the typical kite at rounding level
-    (median < 1e-8); returns the worst kite's error."""
+    sensitivity envelope COND_ENVELOPE, at most one kite in a thousand (and
+    one in any smaller batch) above RTI_TOL, the typical kite at rounding
+    level (median < 1e-8); returns the worst kite's error."""
     e = np.maximum.reduce([rel_per_kite(r["u0"], u0), rel_per_kite(r["traj"], Xo), rel_per_kite(r["ctrl"], Uo)])
     assert e.max() < COND_ENVELOPE, (where, np.sort(e)[-4:])
+    assert np.sum(e >= RTI_TOL) <= max(1, e.size // 1000), (where, np.sort(e)[-4:])
     assert e.size < 8 or np.median(e) < 1e-8, (where, np.median(e))
     return float(e.max())
 
@@ -775,3 +777,40 @@ def test_rk4_sens_hot_kernel_ragged_batch(kp, fp32):
         xr, Ar, Br = ffi.rk4_sens(kp, x[i], u[i], 0.025, 2)
         assert rel(xo[i], xr) < 1e-12, i
         assert rel(A[i], Ar) < stol and rel(Bm[i], Br) < stol, (i, rel(A[i], Ar), rel(Bm[i], Br))
+
+
+@pytest.mark.parametrize("Nh", [20, 40])
+def test_captured_host_step_matches_uncaptured(Nh):
+    """kite_nmpc_step runs a captured HIP graph with pinned staging (batch-1
+    latency); KITE_NMPC_NO_GRAPH=1 keeps the plain launch
+    sequence.  Both give bitwise the same closed loop, through a cold restart
+    (reset: the cold graph), new bounds mid-loop (re-capture) and a
+    set_solution warm start."""
+    import os
+    B = 3
+    x0 = x0_batch(B, offset=3300)
+    cfg = ok.default_config(N=Nh)
+    os.environ["KITE_NMPC_NO_GRAPH"] = "1"
+    try:
+        gp = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    finally:
+        del os.environ["KITE_NMPC_NO_GRAPH"]
+    gg = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    try:
+        xp, xg = x0.copy(), x0.copy()
+        ubx = np.array(cfg.ubx); ubx[3:6] = 3.0
+        for step in range(7):
+            if step == 3:
+                gp.set_bounds(ubx=ubx); gg.set_bounds(ubx=ubx)
+            if step == 5:
+                gp.reset(); gg.reset()
+            if step == 6:
+                Xs, Us = gp.get_solution()
+                gp.set_solution(Xs, Us); gg.set_solution(Xs, Us)
+            rp, rg = gp.step(xp), gg.step(xg)
+            for k in ("u0", "traj", "ctrl", "status"):
+                np.testing.assert_array_equal(rp[k], rg[k], err_msg=f"{k} step {step}")
+            np.testing.assert_array_equal(rp["diag"][:, :5], rg["diag"][:, :5])
+            xp, xg = rp["traj"][:, 1, :].copy(), rg["traj"][:, 1, :].copy()
+    finally:
+        gp.close(); gg.close()
