@@ -126,3 +126,33 @@ def test_bench_refuses_more_gpus_than_present():
     assert r.returncode != 0
     assert "GPU" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_measurement_noise_disturbs_the_plant_reproducibly():
+    """bench.py --meas-noise (fleet.MeasurementNoise): the measured state is the
+    plan's node 1 plus seeded noise on the kite states only (theta / thetadot
+    untouched, the attitude renormalised), the same draws for the same seed; with the
+    oracle as the stepper the disturbed loop leaves the nominal one."""
+    from openkite_amd.fleet import MeasurementNoise
+    B = 4
+    runs = []
+    for noise_seed in (None, 5, 5, 6):
+        x0 = initial_states(0, B)
+        noise = None if noise_seed is None else MeasurementNoise(1.0, torch.device("cpu"), noise_seed)
+        loop = FleetLoop(OracleStepper(B), x0, N, DT, noise=noise)
+        xs = []
+        for _ in range(2):
+            loop.step()
+            xs.append(loop.x0.clone())
+            traj1 = loop.traj[:, 1, :]
+            np.testing.assert_array_equal(loop.x0[:, 13:].numpy(), traj1[:, 13:].numpy())
+            if noise is not None:
+                np.testing.assert_allclose(loop.x0[:, 9:13].norm(dim=1).numpy(), 1.0, rtol=1e-14)
+                d = (loop.x0[:, :13] - traj1[:, :13]).abs()
+                assert d.max() > 0 and d.max() < 0.5
+            else:
+                np.testing.assert_array_equal(loop.x0.numpy(), traj1.numpy())
+        runs.append(torch.stack(xs))
+    assert torch.equal(runs[1], runs[2])                 # same seed, same draws
+    assert not torch.equal(runs[1], runs[3])             # another seed
+    assert not torch.equal(runs[0], runs[1])             # the noise reaches the loop

@@ -586,8 +586,14 @@ def test_kite_nmpf_facade_reference_order():
     assert d["virt_state"] == X[13, -1]
 
 
+SURVEY_RTI_TOL = 1e-9   # RTI u0 / trajectory, GPU vs CPU, fp64.  The
+                        # ill-conditioned QPs put a few kites above it (their
+                        # envelopes above); the distribution bars below hold the
+                        # bulk of every full-batch loop to it.
+
+
 def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_frac=0.99, max_err=1e-4,
-                               max_diverged=None):
+                               max_diverged=None, survey_frac=None):
     """B = 4096 closed loop: every step starts the GPU from the oracle's previous
     solution (set_solution), so each step is a parity check from identical
     inputs over the whole batch; per-kite errors relative to max(1, |oracle|)."""
@@ -622,7 +628,10 @@ def _loop_vs_oracle_full_batch(kp, cfgv, cfg, steps, tol, offset, label, err_fra
     assert diverged.sum() <= (max_diverged if max_diverged is not None else B // 1000), np.where(diverged)[0]
     e = np.concatenate(errs)
     print(f"{label}: B={B} x {steps} steps, {diverged.sum()} kites with differing safeguard decisions; "
-          f"kite-step errors median {np.median(e):.1e}, p99 {np.quantile(e, 0.99):.1e}, max {e.max():.1e}")
+          f"kite-step errors median {np.median(e):.1e}, p99 {np.quantile(e, 0.99):.1e}, max {e.max():.1e}; "
+          f"{np.mean(e < SURVEY_RTI_TOL):.4f} within SURVEY's 1e-9")
+    if survey_frac is not None:
+        assert np.mean(e < SURVEY_RTI_TOL) >= survey_frac, (label, np.mean(e < SURVEY_RTI_TOL))
 
 
 def test_config3_full_batch_vs_oracle(kp, cfgv):
@@ -631,7 +640,9 @@ def test_config3_full_batch_vs_oracle(kp, cfgv):
     # measured (r03c): median 1.7e-10, p99 2.3e-9, max 2.6e-6, no differing safeguard
     # decision -- so >= 99.9 % of the kites at the RTI bar each step, every one
     # inside the condensed QP's sensitivity envelope
-    _loop_vs_oracle_full_batch(kp, cfgv, ok.default_config(), 3, RTI_TOL, 9000, "config 3 fp64", err_frac=0.999)
+    # and >= 95 % of the kite-steps at SURVEY 8(c)'s 1e-9 (measured: p99 2.2e-9, median 1.6e-10)
+    _loop_vs_oracle_full_batch(kp, cfgv, ok.default_config(), 3, RTI_TOL, 9000, "config 3 fp64", err_frac=0.999,
+                               survey_frac=0.95)
 
 
 def test_config4_fp32_sensitivities_full_batch_vs_fp64_oracle(kp, cfgv):
@@ -711,6 +722,9 @@ def _config5_vs_oracle(kp, B, steps, offset):
             orc_rows += int(_rows_outside(node, Xo).sum())
         assert np.all(np.isfinite(loop.traj.cpu().numpy()))
         assert frozen_total >= 0.9 * B * steps, frozen_total
+    # SURVEY 8(c)'s 1e-9 for >= 99.9 % of the kite-steps (measured p99.9: 5.5e-10)
+    ea = np.concatenate(errs)
+    assert np.mean(ea < SURVEY_RTI_TOL) >= 0.999, np.mean(ea < SURVEY_RTI_TOL)
         assert rejected <= B * steps // 200, rejected     # the oracle's 512 x 23 loop: 2 of 11 776
         assert flipped <= max(1, B * steps // 1000), flipped
         b_steps, b_rows = g.state_bound_stats()
@@ -814,3 +828,28 @@ def test_captured_host_step_matches_uncaptured(Nh):
             xp, xg = rp["traj"][:, 1, :].copy(), rg["traj"][:, 1, :].copy()
     finally:
         gp.close(); gg.close()
+
+
+@pytest.mark.parametrize("Nh", [20, 40])
+def test_timing_reports_the_main_qp_kernel(Nh):
+    """API 6: kernel_times / timing_read carry a sixth entry, the main QP kernel
+    alone (bench.py's roofline kernel), inside the QP phase, which also holds
+    the expansion and the lazy-row launch at N = 20."""
+    B = 64
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(N=Nh, timing=1), B)
+    try:
+        x = x0_batch(B)
+        for _ in range(2):
+            x = g.step(x)["traj"][:, 1, :].copy()
+        kt = g.kernel_times()
+        assert set(kt) == set(ok.BatchNMPC.TIMING_KEYS)
+        assert 0.0 < kt["qp_main"] <= kt["qp"] <= kt["total"]
+        g.timing_start(3)
+        for _ in range(3):
+            x = g.step(x)["traj"][:, 1, :].copy()
+        n, ks = g.timing_read()
+        assert n == 3
+        assert 0.0 < ks["qp_main"] <= ks["qp"] <= ks["total"]
+        assert abs(ks["prologue"] + ks["rk4_sens"] + ks["condense"] + ks["qp"] - ks["total"]) < 1e-3 * ks["total"] + 1e-3
+    finally:
+        g.close()
