@@ -42,8 +42,11 @@ METRIC = "NMPC RTI steps/sec, batch=4096 N=20 horizon, 1/2/4/8 MI355X"
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 30 + 3 steps: the synthetic fleet is a transient from the launch state; in
+    # the nominal loop kites start to fail from step ~45 on, in the oracle
+    # exactly as on the GPU (profiles/r05j_oracle_long_loop.txt)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--substeps", type=int, default=2)
@@ -64,6 +67,16 @@ def parse(argv=None):
                     help="disturbed plant: seeded Gaussian noise on every measured state (body velocity and rates "
                          "0.05 S, position 0.01 S, attitude ~0.01 S rad; openkite_amd/fleet.py MeasurementNoise), "
                          "so the controller's model no longer predicts the plant exactly; 0 = the nominal loop")
+    ap.add_argument("--rate-bound", type=float, default=0.0, metavar="W",
+                    help="binding state box: |omega_i| <= W rad/s on every node instead of the reference's 4 pi "
+                         "(nmpf_node.cpp:59-63, never active on this workload); the condensed QP enforces it with "
+                         "lazy rows, the multiple-shooting QP (--qp-kernel 3) with soft rows on every node; 0 = the "
+                         "reference bounds")
+    ap.add_argument("--qp-lm", type=float, default=None,
+                    help="qp_kernel 3: Levenberg-Marquardt term (default: the config's 10); 0 with --soft-weight 1e6 "
+                         "at N = 20 is the undamped every-node mode (DESIGN 2.1)")
+    ap.add_argument("--soft-weight", type=float, default=None,
+                    help="qp_kernel 3: exact-L1 weight of the state rows (default: the config's 1e3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline sample")
     ap.add_argument("--latency-steps", type=int, default=1000,
@@ -117,6 +130,7 @@ def gpu_single_kite_latency(args, ok, x1, steps=200, warm=20):
     cfg = ok.default_config(N=args.horizon, M=args.substeps, qp_iters=args.qp_iters)
     cfg.qp_kernel = args.qp_kernel
     cfg.sens_fp32 = 1 if args.fp32_sens else 0
+    apply_qp_options(cfg, args)
     g = ok.BatchNMPC(ok.load_properties(), cfg, 1)
     try:
         x = x1.copy()
@@ -131,6 +145,37 @@ def gpu_single_kite_latency(args, ok, x1, steps=200, warm=20):
         g.close()
     return {"median_ms": round(float(np.median(t)), 4), "p90_ms": round(float(np.percentile(t, 90)), 4),
             "steps": steps, "api": "kite_nmpc_step (host arrays, synchronous)"}
+
+
+def apply_qp_options(cfg, args):
+    """--rate-bound, --qp-lm, --soft-weight on a context config or on the
+    oracle's node_config dict (which also takes the QP form of --qp-kernel)."""
+    apply_rate_bound(cfg, args.rate_bound)
+    if isinstance(cfg, dict):
+        import openkite_amd as ok
+        if ok.resolve_qp_kernel(args.qp_kernel, args.horizon) == 3:
+            cfg["qp_form"] = 1
+        if args.qp_lm is not None:
+            cfg["lm"] = args.qp_lm
+        if args.soft_weight is not None:
+            cfg["soft_weight"] = args.soft_weight
+    else:
+        if args.qp_lm is not None:
+            cfg.qp_lm = args.qp_lm
+        if args.soft_weight is not None:
+            cfg.qp_soft_weight = args.soft_weight
+    return cfg
+
+
+def apply_rate_bound(cfg, w):
+    """--rate-bound: |omega_i| <= w on the states 3..5 of every node (a config
+    object or the oracle's node_config dict); w <= 0 keeps the reference box."""
+    if w <= 0.0:
+        return cfg
+    lb, ub = (cfg["lbx"], cfg["ubx"]) if isinstance(cfg, dict) else (cfg.lbx, cfg.ubx)
+    for i in range(3, 6):
+        lb[i], ub[i] = -w, w
+    return cfg
 
 
 def host_cpu_info():
@@ -173,7 +218,7 @@ def cpu_baseline(args, x0_host, budget_s, wind=None):
     # one-GPU job (nproc shows the whole machine); else this process's CPU set
     threads = info["omp_num_threads"] or info["affinity_cpus"] or os.cpu_count() or 1
     kp = ffi.load_params()
-    cfgv = ffi.cfg_vector(ffi.node_config(N=args.horizon))
+    cfgv = ffi.cfg_vector(apply_qp_options(ffi.node_config(N=args.horizon), args))
     N = args.horizon
     S = min(x0_host.shape[0], 64 * threads)
     x = x0_host[:S].copy()
@@ -223,6 +268,12 @@ def run_config_tag(args):
         tag["wind_sweep"] = args.wind_sweep
     if args.meas_noise > 0.0:
         tag["meas_noise"] = args.meas_noise
+    if args.rate_bound > 0.0:
+        tag["rate_bound"] = args.rate_bound
+    if args.qp_lm is not None:
+        tag["qp_lm"] = args.qp_lm
+    if args.soft_weight is not None:
+        tag["soft_weight"] = args.soft_weight
     return tag
 
 
@@ -353,6 +404,7 @@ def main():
     cfg = ok.default_config(N=N, M=args.substeps, qp_iters=args.qp_iters, device=local)
     cfg.qp_kernel = args.qp_kernel
     cfg.sens_fp32 = 1 if args.fp32_sens else 0
+    apply_qp_options(cfg, args)
     ctx = ok.BatchNMPC(ok.load_properties(), cfg, B)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
@@ -441,10 +493,14 @@ def main():
         workload = (f"batch={B}/GPU, N={N}, M={args.substeps}, full RTI fp64"
                     + (", fp32 sensitivities (BASELINE configs[3] precision)" if args.fp32_sens else "")
                     + (" + fused EKF (BASELINE configs[4])" if args.ekf else
-                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens and wind is None and noise is None else "")
+                       " (BASELINE configs[2])" if N == 20 and not args.fp32_sens and wind is None and noise is None
+                       and args.rate_bound <= 0.0 and args.qp_lm is None and args.soft_weight is None else "")
                     + (f", wind-field sweep |W_h| <= {args.wind_sweep} m/s per instance (build extension)"
                        if wind is not None else "")
-                    + (f", disturbed plant: measurement noise S = {args.meas_noise}" if noise is not None else ""))
+                    + (f", disturbed plant: measurement noise S = {args.meas_noise}" if noise is not None else "")
+                    + (f", binding state box |omega_i| <= {args.rate_bound} rad/s" if args.rate_bound > 0.0 else "")
+                    + (f", multiple-shooting QP lm = {cfg.qp_lm:g}, soft weight {cfg.qp_soft_weight:g}"
+                       if args.qp_lm is not None or args.soft_weight is not None else ""))
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -462,7 +518,9 @@ def main():
                        "batch_per_gpu": B, "global_batch": world * B, "horizon_N": N, "rk4_substeps": args.substeps,
                        "qp_iter_cap": args.qp_iters, "parallelism": f"dp{world}",
                        "allgather": pub is not None, "wind_sweep_mps": args.wind_sweep,
-                       "meas_noise": args.meas_noise,
+                       "meas_noise": args.meas_noise, "rate_bound": args.rate_bound,
+                       "qp_kernel": ok.resolve_qp_kernel(args.qp_kernel, N), "qp_lm": cfg.qp_lm,
+                       "qp_soft_weight": cfg.qp_soft_weight,
                        "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -477,7 +535,8 @@ def main():
             "status_nan": int(np.sum(status & 1)),
             "state_bounds": {"kite_steps_outside": b_steps, "rows_outside": b_rows,
                              "kite_steps": B * args.steps,
-                             "note": "over the timed steps: committed plans leaving the state box |omega_i| <= 4 pi, "
+                             "note": "over the timed steps: committed plans leaving the state box |omega_i| <= "
+                                     + (f"{args.rate_bound}" if args.rate_bound > 0.0 else "4 pi") + ", "
                                      "|q_i| <= 1.01 (nmpf_node.cpp:59-63; status bit 8) and their (node, state) pairs "
                                      "outside it" + ("; multiple-shooting QP: soft rows with xi > 0 at the accepted "
                                                      "solution" if ok.resolve_qp_kernel(args.qp_kernel, N) == 3

@@ -142,7 +142,10 @@ typedef struct kite_nmpc_config {
                               40 = 2 z0 (the IPM's start multiplier, so every soft row starts
                               dual feasible): smaller values give KITE_EINVAL (since API 5)    */
     double qp_lm;          /* qp_kernel 3: Levenberg-Marquardt term lm/2 ||step||^2 on every QP
-                              variable, scaled units (10); leaves the RTI fixed point unchanged */
+                              variable, scaled units (10); leaves the RTI fixed point unchanged.
+                              qp_lm = 0 with qp_soft_weight = 1e6 at N = 20: the condensed
+                              QP's own step with the state box exact on every node
+                              (DESIGN.md 4.4); at N = 40 the undamped step diverges        */
     /* Arbitrary closed path (KiteNMPF(kite, path), kiteNMPF.h:14, takes any
      * casadi::Function theta -> R^3): with path_harmonics = K in 1..8 the
      * unrotated curve is the truncated Fourier series

@@ -50,3 +50,28 @@ def test_launch_ranks_never_initialises_hip(tmp_path):
     calls.clear()
     assert bench.launch_ranks(types.SimpleNamespace(gpus=8), count=lambda: 1, call=lambda c, env: calls.append(c)) == 2
     assert not calls
+
+
+def test_rate_bound_option_sets_the_box_on_both_sides():
+    """--rate-bound W sets |omega_i| <= W in the context config and in the CPU
+    baseline's oracle config alike, and is part of the run tag the PMC lookup
+    matches on; 0 keeps the reference box."""
+    import openkite_amd as ok
+    from oracle import ffi
+    args = bench.parse(["--rate-bound", "3", "--qp-kernel", "3"])
+    cfg = bench.apply_rate_bound(ok.default_config(N=20), args.rate_bound)
+    assert [cfg.lbx[i] for i in range(3, 6)] == [-3.0] * 3 and [cfg.ubx[i] for i in range(3, 6)] == [3.0] * 3
+    d = bench.apply_rate_bound(ffi.node_config(N=20), args.rate_bound)
+    assert list(d["lbx"][3:6]) == [-3.0] * 3 and list(d["ubx"][3:6]) == [3.0] * 3
+    assert bench.run_config_tag(args)["rate_bound"] == 3.0
+    ref = ok.default_config(N=20)
+    assert bench.apply_rate_bound(ok.default_config(N=20), 0.0).ubx[3] == ref.ubx[3]
+    assert "rate_bound" not in bench.run_config_tag(bench.parse([]))
+    # the undamped every-node mode reaches both the context and the baseline
+    a2 = bench.parse(["--qp-kernel", "3", "--qp-lm", "0", "--soft-weight", "1e6"])
+    c2 = bench.apply_qp_options(ok.default_config(N=20), a2)
+    assert c2.qp_lm == 0.0 and c2.qp_soft_weight == 1e6
+    d2 = bench.apply_qp_options(ffi.node_config(N=20), a2)
+    assert d2["qp_form"] == 1 and d2["lm"] == 0.0 and d2["soft_weight"] == 1e6
+    assert bench.apply_qp_options(ffi.node_config(N=20), bench.parse([]))["qp_form"] == 0
+    assert bench.run_config_tag(a2)["qp_lm"] == 0.0

@@ -65,6 +65,28 @@ def test_oracle_lazy_rows_enforce_tight_rate_bound(kp):
     assert kept <= active // 4, (kept, active)         # and the rows enforce it
 
 
+def test_oracle_ms_qp_holds_every_node(kp):
+    """The multiple-shooting QP (qp_form 1; GPU qp_kernel 3 at any horizon)
+    carries the state box on every node as exact-L1 soft rows, so on the same
+    closed loop as above no committed plan leaves the tight box (the condensed
+    QP's four lazy rows per round leave a few kite-steps with bit 8)."""
+    N, B = 20, 64
+    outside = {}
+    for form in (0, 1):
+        c = tight_config(N)
+        c["qp_form"] = form
+        cv = ffi.cfg_vector(c)
+        x = x0_batch(B, cv, 11000)
+        Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+        outside[form] = 0
+        for step in range(8):
+            _, _, st = ffi.rti_step(kp, cv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            assert not np.any(st & 32)                 # no rejected steps
+            outside[form] += int((~within_bound(Xo)).sum())
+            x = Xo[:, 1, :].copy()
+    assert outside[1] == 0 and outside[0] > 0, outside
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,qp_kernel", [(20, 1), (20, 2), (40, 1), (40, 2)])
 def test_gpu_lazy_rows_vs_oracle(kp, N, qp_kernel):
@@ -190,3 +212,87 @@ def test_gpu_ms_qp_tight_bounds_vs_oracle(kp, N, extra):
     assert active > 0                                  # the tight box binds
     print(f"N={N} extra={extra}: {frozen} frozen QPs, {active} kite-steps at the tight rate bound, "
           f"max frozen error {e.max():.1e}")
+
+
+# Every-node exact state bounds at the reference's (undamped) step: the
+# multiple-shooting QP with qp_lm = 0 and a soft weight far above any
+# multiplier is the condensed QP of the same RTI step (the state variables
+# eliminated or kept) plus the state box on every node, exact while the
+# linearised box is feasible.  At N = 20 it runs the nominal loop cleanly; at
+# N = 40 the undamped Gauss-Newton step does not.
+EXACT_SOFT_WEIGHT = 1e6
+# Same QP in two formulations, each frozen at a relative 1e-10 on cond ~ 1e11:
+# the kite controls agree to ~1e-6, Uv (weight W = 1e-3 on the speed error,
+# the weakest-determined variable) to ~1e-3 absolute
+FORM_CTRL_TOL = 1e-5
+FORM_UV_TOL = 5e-3
+
+
+def exact_ms_config(N, tight=False):
+    c = tight_config(N) if tight else ffi.node_config(N=N)
+    c["qp_form"] = 1
+    c["lm"] = 0.0
+    c["soft_weight"] = EXACT_SOFT_WEIGHT
+    return c
+
+
+def test_oracle_undamped_ms_qp_is_the_condensed_step(kp):
+    """qp_form 1 at lm = 0, soft weight 1e6 against the condensed QP (qp_form
+    0) on the same first RTI step of 8 kites (vx bound active): the same plan
+    within the two IPMs' freeze envelope."""
+    N, B = 20, 8
+    out = {}
+    for form, c in ((0, ffi.node_config(N=N)), (1, exact_ms_config(N))):
+        c["qp_form"] = form
+        cv = ffi.cfg_vector(c)
+        x = x0_batch(B, cv, 11000)
+        X = np.zeros((B, N + 1, 15)); U = np.zeros((B, N, 4))
+        _, d, st = ffi.rti_step(kp, cv, N, M, K, x, X, U, warm=0)
+        assert not np.any(st & (1 | 2 | 32)) and d[:, 5].max() < 1e-10
+        out[form] = (X, U)
+    dU = np.abs(out[0][1] - out[1][1]).max(axis=(0, 1))
+    assert dU[:3].max() < FORM_CTRL_TOL and dU[3] < FORM_UV_TOL, dU
+    assert np.abs(out[0][0] - out[1][0]).max() < FORM_UV_TOL
+
+
+@pytest.mark.gpu
+def test_gpu_undamped_ms_qp_every_node_vs_oracle(kp):
+    """The every-node mode on the GPU (qp_kernel 3, qp_lm = 0, soft weight 1e6)
+    with the binding |omega_i| <= 3 box, from identical inputs every step:
+    status words equal (bit 2 aside), frozen QPs within the MS envelope, no
+    committed plan outside the box."""
+    N, B, steps = 20, 64, 6
+    c = exact_ms_config(N, tight=True)
+    cv = ffi.cfg_vector(c)
+    cfg = ok.default_config(N=N)
+    cfg.qp_kernel = 3
+    cfg.qp_lm = 0.0
+    cfg.qp_soft_weight = EXACT_SOFT_WEIGHT
+    for i in range(15):
+        cfg.lbx[i], cfg.ubx[i] = c["lbx"][i], c["ubx"][i]
+    x = x0_batch(B, cv, 11000)
+    g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+    Xo = np.zeros((B, N + 1, 15)); Uo = np.zeros((B, N, 4))
+    frozen, errs = 0, []
+    try:
+        for step in range(steps):
+            if step > 0:
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            _, diag, st = ffi.rti_step(kp, cv, N, M, K, x, Xo, Uo, warm=int(step > 0))
+            np.testing.assert_array_equal(r["status"] & ~2, st & ~2, err_msg=f"step {step}")
+            e = np.array([max(abs(r["traj"][k] - Xo[k]).max() / max(1.0, abs(Xo[k]).max()),
+                              abs(r["ctrl"][k] - Uo[k]).max() / max(1.0, abs(Uo[k]).max())) for k in range(B)])
+            conv = (g.qp_stats()[0] < 1e-10) & (diag[:, 5] < 1e-10)
+            assert e[conv].max(initial=0.0) < MS_ENVELOPE, (step, np.sort(e[conv])[-4:])
+            assert e[~conv].max(initial=0.0) < MS_CAP_TOL, (step, np.sort(e[~conv])[-4:])
+            assert np.all(within_bound(r["traj"])[(r["status"] & 32) == 0])
+            errs.append(e[conv])
+            frozen += int(conv.sum())
+            x = Xo[:, 1, :].copy()
+    finally:
+        g.close()
+    e = np.concatenate(errs)
+    assert frozen >= B * steps // 2, frozen
+    assert np.mean(e < RTI_TOL) >= 0.99, np.sort(e)[-5:]
+    print(f"undamped every-node MS QP: {frozen} frozen QPs, max frozen error {e.max():.1e}")
