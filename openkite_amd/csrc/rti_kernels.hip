@@ -755,11 +755,36 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
 // The three columns past the control block (theta0, thetadot0 and the
 // affine residual column that yields the gradient) are accumulated on the
 // VALU against variable i = l (slot 0) and 64 + l (slot 1): H_ab, H_bb and h
-// come straight out of them.  Small footprint (~14 KB LDS) so two kites share
+// come straight out of them.  Small footprint (~10 KB LDS) so two kites share
 // a SIMD (launch bound 2 waves / SIMD).
 //   lane t < 60 : column t of G (kite control (k = t/3, c = t%3)), 13 rows in VGPRs
 //   lane 60     : the affine column g (propagated defects)
+// The propagation G_{k+1} = A_k G_k needs every element of A_k in every lane.
+// Round 5 moved it from LDS broadcast reads (169 ds_read_b64 per node and
+// kite, 86 KB of LDS return traffic: the CU's LDS was the kernel's bound) to
+// register-resident columns broadcast inside the FMA (fmac_col13): 0.184 ->
+// 0.140 ms, bitwise the same output (profiles/r05l_condense_dpp_ab.txt).
 // ---------------------------------------------------------------------------
+// nv[i] += A[i][j] * v_j for the 13 rows i of one column j, the column held in
+// ONE register in row layout (lane p of every 16-lane row holds A[p][j]):
+// v_fmac_f64_dpp with row_newbcast:i broadcasts A[i][j] to the whole row
+// inside the FMA -- no LDS broadcast read.  The compiler does not form this
+// instruction itself (it keeps a v_mov_b64_dpp + v_fmac_f64 pair), and its
+// hazard recognizer does not look into inline asm: the leading s_nop 1 covers
+// the two wait states a VALU write of the DPP source needs (the column comes
+// from a global load, but the register allocator may copy it).
+#define KITE_FMAC_DPP(I) "v_fmac_f64_dpp %" #I ", %13, %14 row_newbcast:" #I " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ void fmac_col13(double (&nv)[NK], double a, double vj) {
+    asm("s_nop 1\n\t"
+        KITE_FMAC_DPP(0) KITE_FMAC_DPP(1) KITE_FMAC_DPP(2) KITE_FMAC_DPP(3) KITE_FMAC_DPP(4)
+        KITE_FMAC_DPP(5) KITE_FMAC_DPP(6) KITE_FMAC_DPP(7) KITE_FMAC_DPP(8) KITE_FMAC_DPP(9)
+        KITE_FMAC_DPP(10) KITE_FMAC_DPP(11) KITE_FMAC_DPP(12)
+        : "+v"(nv[0]), "+v"(nv[1]), "+v"(nv[2]), "+v"(nv[3]), "+v"(nv[4]), "+v"(nv[5]), "+v"(nv[6]),
+          "+v"(nv[7]), "+v"(nv[8]), "+v"(nv[9]), "+v"(nv[10]), "+v"(nv[11]), "+v"(nv[12])
+        : "v"(a), "v"(vj));
+}
+#undef KITE_FMAC_DPP
+
 constexpr int CD20_N = 20, CD20_NA = 80, CD20_n = 82;
 constexpr int CD20_WLD = 112;                    // Wc row stride: 2*WLD % 64 == 32 -> conflict-free tile reads
 __global__ __launch_bounds__(64, 2) void k_condense20(RtiConst C, int B, const double* __restrict__ X,
@@ -771,8 +796,6 @@ __global__ __launch_bounds__(64, 2) void k_condense20(RtiConst C, int B, const d
                                                       double* __restrict__ Htl, double* __restrict__ Hab,
                                                       double* __restrict__ Hbb) {
     constexpr int N = CD20_N, n = CD20_n, NA = CD20_NA, WLD = CD20_WLD;
-    constexpr int SAL = 16 * 16 + NK + 3;
-    __shared__ double sA[2][SAL];                    // [A_k | B_k] column-major (col j: 16 j + i), then d_k
     __shared__ double Wc[4 * WLD];                   // the 4 residual rows of the current node
     __shared__ double sX[(N + 1) * NX];
     __shared__ double sPth[N + 1][6];
@@ -844,40 +867,33 @@ __global__ __launch_bounds__(64, 2) void k_condense20(RtiConst C, int B, const d
         if (l < 96 - 64) sHx[c][64 + l] = 0.0;
     }
 
-    // interval data PD nodes ahead in a register ring (221 doubles -> 4 per lane)
-    constexpr int NPF = (NK * 16 + NK + 63) / 64;
-    constexpr int PD = 1;
-    double pf[PD][NPF];
-    auto load_iv = [&](int k, double* dst) __attribute__((always_inline)) {
+    // interval data of the next node in registers, row layout: lane l holds row
+    // p = l & 15 of [A_k | B_k] (Ar[j], j < 16) and d_k[p] (Ar[16]); rows 13..15
+    // repeat row 12 and are never read (the broadcasts take lanes 0..12).  Loaded
+    // right after the previous node's propagation, consumed by the next one: the
+    // node's fold runs in between.
+    typedef double double2v __attribute__((ext_vector_type(2)));
+    double Ar[16 + 1];
+    auto load_ar = [&](int k) __attribute__((always_inline)) {
+        const int p = min(l & 15, NK - 1);
+        const double2v* src = reinterpret_cast<const double2v*>(ABb + (size_t)k * NK * 16 + (size_t)p * 16);
 #pragma unroll
-        for (int q = 0; q < NPF; ++q) {
-            const int e = l + 64 * q;
-            double val = 0.0;
-            if (e < NK * 16) val = ABb[(size_t)k * NK * 16 + e];
-            else if (e < NK * 16 + NK) val = DEFb[(size_t)k * NK + (e - NK * 16)];
-            dst[q] = val;
+        for (int q = 0; q < 8; ++q) {
+            const double2v t2 = src[q];
+            Ar[2 * q] = t2[0];
+            Ar[2 * q + 1] = t2[1];
         }
+        Ar[16] = DEFb[(size_t)k * NK + p];
     };
-#pragma unroll
-    for (int q = 0; q < PD; ++q) load_iv(q, pf[q]);
+    load_ar(0);
     double wpD[3], wpT[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) { wpD[a] = C.sqQ_dt[a] * C.Sr[a]; wpT[a] = C.sqQ_T[a] * C.Sr[a]; }
     double* Crb = Cr + (size_t)b * N * n;
 
-    auto node = [&](int k, double* pfs) __attribute__((always_inline)) {
+    auto node = [&](int k) __attribute__((always_inline)) {
         const bool last = (k == N);
-        const int par = k & 1;
-        if (!last) {
-#pragma unroll
-            for (int q = 0; q < NPF; ++q) {
-                const int e = l + 64 * q;
-                if (e < NK * 16) sA[par][(e & 15) * 16 + (e >> 4)] = pfs[q];       // transpose: column-major
-                else if (e < NK * 16 + NK) sA[par][16 * 16 + (e - NK * 16)] = pfs[q];
-            }
-        }
-        wave_sync();                  // sA[par] visible; the previous node's Wc reads are done
-        if (k + PD < N) load_iv(k + PD, pfs);
+        wave_sync();                  // the previous node's Wc reads are done
         // the affine column at node k, wave-uniform (lane 60)
         const double g0 = uniform_d(readlane_d(v[0], 3 * N));
         const double gr0 = uniform_d(readlane_d(v[6], 3 * N));
@@ -970,38 +986,29 @@ __global__ __launch_bounds__(64, 2) void k_condense20(RtiConst C, int B, const d
             }
         }
         if (!last) {
-            // G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k
-            const double* sa = sA[par];
-            if ((kite_lane && k >= kb) || aff_lane) {
-                double nv[NK];
-                if (kite_lane && k == kb) {
+            // G_{k+1} = A_k G_k (+ B_k e_c at k == kb), g_{k+1} = A_k g_k + d_k as
+            // one product [A_k | B_k | d_k] [v; e_c at k == kb; 1 on the affine
+            // lane], every lane (DPP needs the whole wave; a lane before its
+            // start node has v = 0 and stays at +0).  Same terms in the same
+            // order as round 4's LDS form (d first, then A column by column;
+            // the B terms add exact zeros except at k == kb, where v = 0 and
+            // the B column is the value): bitwise the same up to signed zeros.
+            double nv[NK];
 #pragma unroll
-                    for (int i = 0; i < NK; ++i) nv[i] = sa[(NK + cc) * 16 + i];
-                } else {
-                    const double am = aff_lane ? 1.0 : 0.0;
+            for (int i = 0; i < NK; ++i) nv[i] = 0.0;
+            const bool start = kite_lane && k == kb;
+            fmac_col13(nv, Ar[16], aff_lane ? 1.0 : 0.0);
 #pragma unroll
-                    for (int i = 0; i < NK; ++i) nv[i] = am * sa[16 * 16 + i];
-                    // column-oriented, one column of A_k in registers at a
-                    // time (the memory clobber keeps the compiler from
-                    // hoisting all 169 LDS loads into registers)
+            for (int j = 0; j < NK; ++j) fmac_col13(nv, Ar[j], v[j]);
 #pragma unroll
-                    for (int j = 0; j < NK; ++j) {
-                        double ac[NK];
+            for (int c = 0; c < NKU; ++c) fmac_col13(nv, Ar[NK + c], (start && cc == c) ? 1.0 : 0.0);
 #pragma unroll
-                        for (int i = 0; i < NK; ++i) ac[i] = sa[j * 16 + i];
-                        const double vj = v[j];
-#pragma unroll
-                        for (int i = 0; i < NK; ++i) nv[i] = fma(ac[i], vj, nv[i]);
-                        asm volatile("s_nop 0" ::: "memory");
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < NK; ++i) v[i] = nv[i];
-            }
+            for (int i = 0; i < NK; ++i) v[i] = nv[i];
+            if (k + 1 < N) load_ar(k + 1);
         }
     };
 #pragma unroll 1
-    for (int k = 0; k <= N; ++k) node(k, pf[0]);
+    for (int k = 0; k <= N; ++k) node(k);
 
     // scaled QP out: H_aa tiles (+ R diagonal) in the tiled QP's lane order,
     // H_ab / H_bb / h from the three extra columns; hmax = max |H|
