@@ -13,6 +13,8 @@ mpmath at 50 significant digits.  It pins:
   * Chebyshev-Gauss-Lobatto D, Clenshaw-Curtis weights, composite D and the
     Chebyshev expansion (chebyshev.hpp:113-232, kitemath.h:50-72)
   * the path P(theta) and dP/dtheta
+  * the collocation residual G and cost J of the reference's full_generics
+    test NLP at its own 209-vector (chebyshev.hpp:241-333)
 
 Inputs are the known-answer states of the reference tests plus
 seeded perturbations of the in-flight state of launch/simulator.launch:3.
@@ -301,11 +303,54 @@ def main():
         Pm = Pf(mp.mpf(tv)); dPm = dPf(mp.mpf(tv))
         path.append(dict(theta=tv, P=[float(Pm[i]) for i in range(3)], dP=[float(dPm[i]) for i in range(3)]))
 
+    # ---- collocation residual and cost at the reference test's NLP point ------
+    # kite_control_test.cpp:455-526 (full_generics_test): one segment of order
+    # 10 on [0, 1], unscaled, path radius 3 rotated by q = (cos pi/24, 0,
+    # sin pi/24, 0), Q = 1e-2 diag(1e4, 1e4, 5e3), W = 1e-3, vref = 0.05, no R
+    # term, Mayer 2Q on node 0; the 209-vector ARG["x0"] of :582-598.
+    # CollocateDynamics (chebyshev.hpp:241-271): G = (CompDiff (x) I15) X -
+    # t_scale F(X_i, U_i), t_scale = (tf - t0) / (2 S); CollocateCost (:280-333):
+    # Mayer(X_0) + t_scale sum_m w_m L(X_m, U_m).
+    fix = json.load(open(os.path.join(HERE, "colloc_full_generics.json")))
+    zc = to_mp(fix["z"])
+    Pn, Sn = 10, 1
+    nn = Pn * Sn + 1
+    Xc = [zc[15 * i:15 * i + 15] for i in range(nn)]
+    Uc = [zc[15 * nn + 4 * i:15 * nn + 4 * i + 4] for i in range(nn)]
+    CDc = comp_D(Pn, Sn)
+    tsc = mp.mpf(1) / (2 * Sn)
+    Gc = []
+    for i in range(nn):
+        Fi = aug_f(Xc[i], Uc[i])
+        for r in range(15):
+            Gc.append(mp.fsum(CDc[i][j] * Xc[j][r] for j in range(nn)) - tsc * Fi[r])
+    qc = [sp.cos(sp.pi / 24), 0, sp.sin(sp.pi / 24), 0]
+    Pcq = qmul(qmul(qinv(qc), [0, 3 * sp.cos(th), 3 * sp.sin(th), 0]), qc)
+    Pcf = sp.lambdify(th, sp.Matrix(Pcq[1:4]), "mpmath")
+    Qc = [mp.mpf(100), mp.mpf(100), mp.mpf(50)]
+    Wc, vrefc = mp.mpf("0.001"), mp.mpf("0.05")
+
+    def path_res(xv):
+        Pm = Pcf(xv[13])
+        return [Pm[a] - xv[6 + a] for a in range(3)]
+
+    def lagr(xv):
+        rr = path_res(xv)
+        return mp.fsum(Qc[a] * rr[a] ** 2 for a in range(3)) + Wc * (vrefc - xv[14]) ** 2
+
+    r0 = path_res(Xc[0])
+    mayer = mp.fsum(2 * Qc[a] * r0[a] ** 2 for a in range(3))
+    wc = cc_weights(Pn)
+    Jc = mayer + tsc * mp.fsum(wc[m] * lagr(Xc[m]) for m in range(nn))
+    colloc = dict(source="kite_control_test.cpp:455-598 full_generics_test; chebyshev.hpp:241-333",
+                  fixture="colloc_full_generics.json", G=mpl(Gc), J=float(Jc), mayer=float(mayer))
+
     out = dict(
         generator="tests/golden/gen_golden.py (sympy %s, mpmath %s, %d digits)" % (sp.__version__, mp.__version__, mp.mp.dps),
         params_file="data/umx_radian.yaml",
         rhs=rhs_cases, rk4=rk4_cases, rk4_reference_call=rk4_ref_call, chebyshev=cheb,
         path=dict(radius=2.65, altitude=0.0, q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0], cases=path),
+        colloc=colloc,
     )
     with open(os.path.join(HERE, "kite_golden.json"), "w") as fobj:
         json.dump(out, fobj, indent=1)

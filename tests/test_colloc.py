@@ -49,6 +49,35 @@ def dense_jacobian(c, blocks):
     return np.hstack([Jx, Ju])
 
 
+GOLD = json.load(open(os.path.join(HERE, "golden", "kite_golden.json")))["colloc"]
+COLLOC_TOL = 1e-12      # relative to max |G| and to J; the 50-digit golden is exact to fp64
+
+
+def test_oracle_colloc_vs_golden(kp):
+    """The oracle's collocation residual and cost at the reference test's own
+    NLP point against an independent 50-digit restatement of
+    CollocateDynamics / CollocateCost (tests/golden/gen_golden.py 'colloc')."""
+    G, J = ffi.colloc_eval(kp, FIX["config"], np.array(FIX["z"]))
+    g = np.array(GOLD["G"])
+    assert np.abs(G[0] - g).max() <= COLLOC_TOL * np.abs(g).max()
+    assert abs(J[0] - GOLD["J"]) <= COLLOC_TOL * abs(GOLD["J"])
+
+
+@pytest.mark.gpu
+def test_gpu_colloc_vs_golden():
+    """The same golden on the GPU evaluator (k_colloc)."""
+    c = FIX["config"]
+    cfg = ok.colloc_default_config(**{k: v for k, v in c.items() if k != "lines"})
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), 1)
+    try:
+        G, J, _ = g.colloc_eval(cfg, np.array(FIX["z"])[None], jac=True)
+    finally:
+        g.close()
+    gg = np.array(GOLD["G"])
+    assert np.abs(G[0] - gg).max() <= COLLOC_TOL * np.abs(gg).max()
+    assert abs(J[0] - GOLD["J"]) <= COLLOC_TOL * abs(GOLD["J"])
+
+
 def test_fixture_is_the_reference_vector():
     z = np.array(FIX["z"])
     assert z.size == 209 and z[0] == 0.322159 and z[-1] == -1.83182
