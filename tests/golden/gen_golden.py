@@ -15,6 +15,8 @@ mpmath at 50 significant digits.  It pins:
   * the path P(theta) and dP/dtheta
   * the collocation residual G and cost J of the reference's full_generics
     test NLP at its own 209-vector (chebyshev.hpp:241-333)
+  * the RTI objective (the reference's Lagrange / Mayer terms with the node's
+    weights and scaling) on the shooting grid at seeded plans
 
 Inputs are the known-answer states of the reference tests plus
 seeded perturbations of the in-flight state of launch/simulator.launch:3.
@@ -345,12 +347,62 @@ def main():
     colloc = dict(source="kite_control_test.cpp:455-598 full_generics_test; chebyshev.hpp:241-333",
                   fixture="colloc_full_generics.json", G=mpl(Gc), J=float(Jc), mayer=float(mayer))
 
+    # ---- the RTI's objective on the shooting grid --------------------------------
+    # The reference's Lagrange and Mayer terms (kiteNMPF.cpp:117-141, scaled
+    # variables: residual = Sx_r P(theta) - x_r, speed term W (vref_s -
+    # x14_s)^2, R u_s^2) with the node's weights, scaling, reference speed and
+    # path (kiteNMPF.cpp:32-34, nmpf_node.cpp:30-68), on the build's grid:
+    # sum_{k<N} dt L(x_k, u_k) + Mayer(x_N), N = 20, dt = 0.05.
+    Qn = [mp.mpf(1000), mp.mpf(1000), mp.mpf(10000)]
+    Rn = [mp.mpf("1e-4"), mp.mpf("0.1"), mp.mpf("0.1"), mp.mpf("1e-3")]
+    Wn = mp.mpf("1e-3")
+    Sxn = [mp.mpf(1) / 10, mp.mpf(1) / 3, mp.mpf(1) / 3, mp.mpf(1) / 2, mp.mpf(1) / 5, mp.mpf(1) / 2,
+           mp.mpf(1) / 3, mp.mpf(1) / 3, mp.mpf(1) / 3, 1, 1, 1, 1, 1 / mp.mpf("6.28"), 1 / mp.mpf("6.28")]
+    Sun = [1 / mp.mpf("0.15"), 1 / mp.mpf("0.2618"), 1 / mp.mpf("0.2618"), mp.mpf(1) / 5]
+    vrefs = Sxn[14] * 4                                    # setReferenceVelocity stores Sx(14,14) v
+    Nr, dtr = 20, mp.mpf("0.05")
+
+    def node_res(xv):                                       # scaled path residual, nmpf path
+        Pm = Pf(xv[13])
+        return [Sxn[6 + a] * Pm[a] - Sxn[6 + a] * xv[6 + a] for a in range(3)]
+
+    rti_cases = []
+    rng_c = np.random.default_rng(777)
+    for case in range(4):
+        Xr = []
+        for k in range(Nr + 1):
+            xv = np.array(base + [0.0, 0.0], dtype=float)
+            xv[0:3] += rng_c.uniform(-1.0, 1.0, 3)
+            xv[3:6] += rng_c.uniform(-0.5, 0.5, 3)
+            xv[6:9] += rng_c.uniform(-0.3, 0.3, 3)
+            xv[9:13] += rng_c.uniform(-0.02, 0.02, 4)
+            xv[13] = rng_c.uniform(-3.0, 3.0)
+            xv[14] = rng_c.uniform(0.0, 5.0)
+            Xr.append([float(t) for t in xv])
+        Ur = [[float(rng_c.uniform(0.1, 0.15)), float(rng_c.uniform(-0.12, 0.12)),
+               float(rng_c.uniform(-0.12, 0.12)), float(rng_c.uniform(-5, 5))] for _ in range(Nr)]
+        Jr = mp.mpf(0)
+        for k in range(Nr + 1):
+            xv = to_mp(Xr[k])
+            rr = node_res(xv)
+            Lk = mp.fsum(Qn[a] * rr[a] ** 2 for a in range(3))
+            if k == Nr:
+                Jr += Lk                                    # Mayer: Q on the path residual only
+            else:
+                uv = to_mp(Ur[k])
+                Lk += Wn * (vrefs - Sxn[14] * xv[14]) ** 2
+                Lk += mp.fsum(Rn[j] * (Sun[j] * uv[j]) ** 2 for j in range(4))
+                Jr += dtr * Lk
+        rti_cases.append(dict(X=Xr, U=Ur, J=float(Jr)))
+    rti_cost = dict(source="kiteNMPF.cpp:117-141 terms, nmpf_node.cpp:30-68 values; build grid N=20 dt=0.05",
+                    cases=rti_cases)
+
     out = dict(
         generator="tests/golden/gen_golden.py (sympy %s, mpmath %s, %d digits)" % (sp.__version__, mp.__version__, mp.mp.dps),
         params_file="data/umx_radian.yaml",
         rhs=rhs_cases, rk4=rk4_cases, rk4_reference_call=rk4_ref_call, chebyshev=cheb,
         path=dict(radius=2.65, altitude=0.0, q=[math.cos(math.pi / 8), 0.0, math.sin(math.pi / 8), 0.0], cases=path),
-        colloc=colloc,
+        colloc=colloc, rti_cost=rti_cost,
     )
     with open(os.path.join(HERE, "kite_golden.json"), "w") as fobj:
         json.dump(out, fobj, indent=1)

@@ -28,6 +28,17 @@ def test_rhs_matches_golden(kp, golden):
         assert rel(ffi.rhs(kp, c["x"], c["u"]), c["f"]) < RHS_TOL, c["source"]
 
 
+def test_rti_cost_matches_golden(golden):
+    """The RTI objective (sum of the squared GN residuals of every node plus
+    the control term, oracle traj_cost) against the reference's Lagrange and
+    Mayer terms restated at 50 digits with the node's weights, scaling,
+    reference speed and path (kiteNMPF.cpp:117-141, nmpf_node.cpp:30-68)."""
+    cv = ffi.cfg_vector(ffi.node_config(N=20))
+    for c in golden["rti_cost"]["cases"]:
+        J = ffi.traj_cost(cv, 20, np.array(c["X"]), np.array(c["U"]))
+        assert abs(J - c["J"]) <= 1e-13 * c["J"], (J, c["J"])
+
+
 @pytest.mark.parametrize("method", ["ad", "cs"])
 def test_jacobian_matches_golden(kp, golden, method):
     for c in golden["rhs"]:
