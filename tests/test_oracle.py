@@ -313,3 +313,39 @@ def test_ms_qp_sensitivity_envelope(kp):
     assert np.mean(np.concatenate([same, moved]) < 1e-6) >= 0.995
     print(f"MS QP envelope: {same.size} same-count solves max {same.max():.1e}, "
           f"{moved.size} with a changed count max {moved.max(initial=0.0):.1e}")
+
+
+@pytest.mark.parametrize("N", [20, 40])
+def test_condensed_qp_is_the_eliminated_ms_qp(kp, N):
+    """Two code paths of the oracle build the same QP: the condensed H, h of
+    build_qp (condensing inside the RK4 sweep) equal the multiple-shooting
+    data of build_msqp (A_k, B_k, d_k, residual rows J_k, r_k, control terms)
+    condensed here in numpy, dx_{k+1} = A_k dx_k + B_k du_k + d_k eliminated,
+    in the same scaled variables w = [du_0 .. du_{N-1}, dtheta_0,
+    dthetadot_0].  Cold-start linearisation points of 4 synthetic kites."""
+    c = ffi.node_config(N=N)
+    cv = ffi.cfg_vector(c)
+    xs = ffi.synthetic_states(4, offset=11000)
+    nu, n = 4, 4 * N + 2
+    for b in range(4):
+        x0 = np.zeros(15); x0[:13] = xs[b]; x0[13] = ffi.closest_point(cv, xs[b, 6:9])
+        _, Xp, Up, _ = ffi.prologue(kp, cv, N, 2, x0, np.zeros((N + 1, 15)), np.zeros((N, 4)), warm=0)
+        q = ffi.build_qp(kp, cv, N, 2, Xp, Up)
+        m = ffi.msqp_build(kp, cv, N, 2, Xp, Up)
+        G = np.zeros((N + 1, 15, n)); g = np.zeros((N + 1, 15))
+        G[0, 13, nu * N] = 1.0; G[0, 14, nu * N + 1] = 1.0
+        for k in range(N):
+            G[k + 1] = m["A"][k] @ G[k]
+            G[k + 1][:, nu * k:nu * k + nu] += m["B"][k]
+            g[k + 1] = m["A"][k] @ g[k] + m["d"][k]
+        H = np.zeros((n, n)); h = np.zeros(n)
+        for k in range(N + 1):
+            nr = 4 if k < N else 3
+            W = m["J"][k, :nr] @ G[k]
+            H += W.T @ W
+            h += W.T @ (m["r"][k, :nr] + m["J"][k, :nr] @ g[k])
+            if k < N:
+                H[nu * k:nu * k + nu, nu * k:nu * k + nu] += np.diag(m["Rh"])
+                h[nu * k:nu * k + nu] += m["rho"][k]
+        assert np.abs(H - q["H"]).max() <= 1e-12 * np.abs(q["H"]).max()
+        assert np.abs(h - q["h"]).max() <= 1e-12 * np.abs(q["h"]).max()
