@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KITE_NMPC_API_VERSION 6   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
+#define KITE_NMPC_API_VERSION 7   /* 2: kite_nmpc_config gained qp_soft_weight, qp_lm;
                                       qp_kernel 3 (multiple-shooting QP, Riccati IPM);
                                    3: kite_nmpc_config gained path_harmonics, path_fourier
                                       (arbitrary closed paths); delay_steps default 16;
@@ -43,7 +43,9 @@ extern "C" {
                                    5: kite_nmpc_set_wind (no config change);
                                       qp_soft_weight must exceed 40 (was 20);
                                    6: kernel_times / timing_read report a sixth
-                                      entry, the main QP kernel alone */
+                                      entry, the main QP kernel alone;
+                                   7: kite_nmpc_timing_start_sampled (events on
+                                      every stride-th step; no config change) */
 #define KITE_PATH_MAX_HARMONICS 8 /* Fourier path: harmonics per axis              */
 
 /* ---- error codes ------------------------------------------------------ */
@@ -328,6 +330,13 @@ int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n);
  * SUMS [ms] in the first min(n, 6) entries of sums_ms:
  * [prologue, rk4_sens, condense, qp, total, qp_main] (as kernel_times).   */
 int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps);
+/* The same ring, recording only every stride-th step from the next one on
+ * (steps 0, stride, 2 stride, ...), at most max_samples of them; timing_read
+ * returns the number recorded.  Each recorded step places six events between
+ * its kernels (~4.6 us each on gfx950); sampling keeps that measurement cost
+ * out of the other steps of a timed run.  stride 1 = kite_nmpc_timing_start
+ * (since API 7).                                                           */
+int kite_nmpc_timing_start_sampled(kite_nmpc_ctx* ctx, int32_t max_samples, int32_t stride);
 int kite_nmpc_timing_read(kite_nmpc_ctx* ctx, double* sums_ms, int32_t n);
 /* QP statistics of the last step: final residual and interior-point
  * iterations per instance (host pointers, B each; either may be NULL).    */

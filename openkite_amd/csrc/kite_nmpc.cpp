@@ -29,6 +29,14 @@ using kite::RtiConst;
 // rows included), and [5] after the main QP kernel alone (k_qp_tiled /
 // k_qp_lds / k_qp / k_qp_ric) -- the roofline's kernel, between [3] and [5]
 constexpr int KITE_NEV = 6;
+// The phase events only time the step: no system-scope fence when they are
+// recorded.  With the default flags every record wrote back and invalidated
+// the caches, 5.6-5.9 us between the kernels it separated (six per step, 2 %
+// of the headline step in profiles/r05m's trace) -- measurement overhead
+// inside the timed region.  Completion is still observable: timing_read
+// synchronises on the last event before reading the elapsed times, and no
+// caller reads device memory through these events.
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 
 struct kite_nmpc_ctx {
     kite_params params;
@@ -72,6 +80,7 @@ struct kite_nmpc_ctx {
     // KITE_NEV events per step
     std::vector<hipEvent_t> ring;
     int ring_cap = 0, ring_used = 0;
+    int ring_stride = 1, ring_phase = 0;   // record every ring_stride-th step
     // kite_nmpc_step's launch sequence (x0 in, every kernel of the step, the
     // outputs out) captured once per warm / cold start into a HIP graph, with
     // pinned host staging: one graph launch and one synchronisation per step
@@ -310,7 +319,9 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     const int B = ctx->B;
     // events: the last-step set (cfg.timing) or the next slot of the ring
     hipEvent_t* ev = nullptr;
-    if (ctx->ring_used < ctx->ring_cap) ev = &ctx->ring[(size_t)ctx->ring_used++ * KITE_NEV];
+    if (ctx->ring_used < ctx->ring_cap) {
+        if (ctx->ring_phase++ % ctx->ring_stride == 0) ev = &ctx->ring[(size_t)ctx->ring_used++ * KITE_NEV];
+    }
     else if (ctx->cfg.timing) ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
@@ -610,7 +621,7 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
         ctx->graph_off = ng && ng[0] == '1';
     }
     for (auto& e : ctx->ev)
-        if (hipEventCreate(&e) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
+        if (hipEventCreateWithFlags(&e, kTimingEventFlags) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
     if (hipDeviceSynchronize() != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_EHIP; }
     *out = ctx;
     return KITE_OK;
@@ -1087,16 +1098,22 @@ int kite_nmpc_kernel_times(kite_nmpc_ctx* ctx, double* ms, int32_t n) {
 }
 
 int kite_nmpc_timing_start(kite_nmpc_ctx* ctx, int32_t max_steps) {
-    if (!ctx || max_steps < 0) return KITE_EINVAL;
+    return kite_nmpc_timing_start_sampled(ctx, max_steps, 1);
+}
+
+int kite_nmpc_timing_start_sampled(kite_nmpc_ctx* ctx, int32_t max_steps, int32_t stride) {
+    if (!ctx || max_steps < 0 || stride < 1) return KITE_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t need = (size_t)max_steps * KITE_NEV;
     while (ctx->ring.size() < need) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&e, kTimingEventFlags));
         ctx->ring.push_back(e);
     }
     ctx->ring_cap = max_steps;
     ctx->ring_used = 0;
+    ctx->ring_stride = stride;
+    ctx->ring_phase = 0;
     // restart the per-instance running sums (ctx->iters[B, 4B))
     HIP_TRY(hipMemsetAsync(ctx->iters + ctx->B, 0, 3 * (size_t)ctx->B * sizeof(int32_t), ctx->stream));
     return KITE_OK;

@@ -154,6 +154,7 @@ _SIGNATURES = {
     "kite_nmpc_kernel_times": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_get_qp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _DP, _DP, _DP, _DP, _DP]),
     "kite_nmpc_timing_start": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "kite_nmpc_timing_start_sampled": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),
     "kite_nmpc_timing_read": (ctypes.c_int, [ctypes.c_void_p, _DP, ctypes.c_int32]),
     "kite_nmpc_qp_stats": (ctypes.c_int, [ctypes.c_void_p, _DP, _IP]),
     "kite_nmpc_qp_iteration_sum": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]),
@@ -348,8 +349,13 @@ class BatchNMPC:
         n = _check(lib().kite_nmpc_kernel_times(self._h, _p(ms), 6), "kernel_times")
         return dict(zip(self.TIMING_KEYS, ms[:n]))
 
-    def timing_start(self, max_steps: int):
-        _check(lib().kite_nmpc_timing_start(self._h, int(max_steps)), "timing_start")
+    def timing_start(self, max_steps: int, stride: int = 1):
+        """Record the kernel events of every stride-th step from the next one
+        on, at most max_steps of them (kite_nmpc_timing_start_sampled)."""
+        if stride == 1:
+            _check(lib().kite_nmpc_timing_start(self._h, int(max_steps)), "timing_start")
+        else:
+            _check(lib().kite_nmpc_timing_start_sampled(self._h, int(max_steps), int(stride)), "timing_start")
 
     def timing_read(self):
         """Per-phase SUMS [ms] over the steps recorded since timing_start

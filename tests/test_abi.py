@@ -41,7 +41,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(ok.MpcDiagnostic) == 6 * 8
     # kite_nmpc_config: 8 int32 + 91 doubles + 2 int32 + 2 int32 + 51 doubles (API 3: Fourier path)
     assert ctypes.sizeof(ok.NmpcConfig) == 12 * 4 + (1 + 3 + 4 + 1 + 15 + 4 + 15 + 15 + 4 + 4 + 1 + 2 + 4 + 2 + 1 + 2 + 51) * 8
-    assert ok.lib().kite_nmpc_api_version() == 6
+    assert ok.lib().kite_nmpc_api_version() == 7
 
 
 @pytest.mark.parametrize("cname,py", [("kite_nmpc_config", "NmpcConfig"), ("kite_colloc_config", "CollocConfig")])

@@ -834,7 +834,8 @@ def test_captured_host_step_matches_uncaptured(Nh):
 def test_timing_reports_the_main_qp_kernel(Nh):
     """API 6: kernel_times / timing_read carry a sixth entry, the main QP kernel
     alone (bench.py's roofline kernel), inside the QP phase, which also holds
-    the expansion and the lazy-row launch at N = 20."""
+    the expansion and the lazy-row launch at N = 20.  API 7: the sampled ring
+    (bench.py records every third timed step)."""
     B = 64
     g = ok.BatchNMPC(ok.load_properties(), ok.default_config(N=Nh, timing=1), B)
     try:
@@ -851,5 +852,16 @@ def test_timing_reports_the_main_qp_kernel(Nh):
         assert n == 3
         assert 0.0 < ks["qp_main"] <= ks["qp"] <= ks["total"]
         assert abs(ks["prologue"] + ks["rk4_sens"] + ks["condense"] + ks["qp"] - ks["total"]) < 1e-3 * ks["total"] + 1e-3
+        # API 7: sampled ring, every third of 7 steps (0, 3, 6) recorded;
+        # the iteration sums still count every step
+        g.timing_start(5, 3)
+        its = 0
+        for _ in range(7):
+            x = g.step(x)["traj"][:, 1, :].copy()
+            its += int(g.qp_stats()[1].sum())
+        n, ks = g.timing_read()
+        assert n == 3
+        assert 0.0 < ks["qp_main"] <= ks["qp"] <= ks["total"]
+        assert g.qp_iteration_sum() == its
     finally:
         g.close()
