@@ -153,15 +153,25 @@ def test_certificate_on_oracle_ms_qp(kp):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [20, 40])
-def test_gpu_ric_solution_satisfies_kkt(kp, N):
+@pytest.mark.parametrize("N,mode", [(20, "default"), (40, "default"), (20, "every_node")])
+def test_gpu_ric_solution_satisfies_kkt(kp, N, mode):
     """The GPU's multiple-shooting QP solutions (k_qp_ric) over 4 closed-loop
     steps of 16 kites satisfy the QP's KKT conditions: stationarity <= 1e-6
     relative (QPs that stopped at the cap K: 1e-4), dynamics and hard bounds to
-    1e-9, soft-bound multipliers within [0, soft_weight]."""
+    1e-9, soft-bound multipliers within [0, soft_weight].  `every_node`: the
+    undamped exact-bound configuration (qp_lm 0, soft weight 1e6)
+    with a binding |omega_i| <= 3 box."""
     B = 16
     c, cv = _cfg(N)
     cfg = ok.default_config(N=N, qp_kernel=3)
+    if mode == "every_node":
+        c["lm"], c["soft_weight"] = 0.0, 1e6
+        c["lbx"][3:6] = [-3.0] * 3
+        c["ubx"][3:6] = [3.0] * 3
+        cv = ffi.cfg_vector(c)
+        cfg.qp_lm, cfg.qp_soft_weight = 0.0, 1e6
+        for i in range(3, 6):
+            cfg.lbx[i], cfg.ubx[i] = -3.0, 3.0
     xs = ffi.synthetic_states(B, offset=8200)
     x = np.zeros((B, 15)); x[:, :13] = xs
     for b in range(B):
@@ -190,4 +200,4 @@ def test_gpu_ric_solution_satisfies_kkt(kp, N):
     finally:
         g.close()
     assert checked >= 3 * B
-    print(f"N={N}: {checked} GPU multiple-shooting QP solutions, stationarity <= {worst:.1e}")
+    print(f"N={N} {mode}: {checked} GPU multiple-shooting QP solutions, stationarity <= {worst:.1e}")
