@@ -319,10 +319,10 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     const int B = ctx->B;
     // events: the last-step set (cfg.timing) or the next slot of the ring
     hipEvent_t* ev = nullptr;
-    if (ctx->ring_used < ctx->ring_cap) {
-        if (ctx->ring_phase++ % ctx->ring_stride == 0) ev = &ctx->ring[(size_t)ctx->ring_used++ * KITE_NEV];
-    }
-    else if (ctx->cfg.timing) ev = ctx->ev;
+    if (ctx->ring_used < ctx->ring_cap && ctx->ring_phase++ % ctx->ring_stride == 0)
+        ev = &ctx->ring[(size_t)ctx->ring_used++ * KITE_NEV];
+    else if (ctx->cfg.timing)
+        ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
     HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, x0, ctx->X, ctx->U, ctx->status,
