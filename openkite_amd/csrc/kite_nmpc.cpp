@@ -55,7 +55,8 @@ struct kite_nmpc_ctx {
     int32_t* status = nullptr;
     int32_t* iters = nullptr;
     int32_t* order = nullptr;      // QP dispatch order (k_qp_order), B entries, then the lazy
-                                   // state-bound list (B + 1: count, kites)
+                                   // state-bound list (B + 1: count, kites), then the
+                                   // prologue's cold-restart list (B + 1)
     // tiled-QP layout (N == 20, 40): H_aa lower tiles [B][NT(NT+1)/2][4][64] with
     // NT = N/4, H_ab [B][4N][2], H_bb [B][2][2]
     bool tiled = false;
@@ -326,7 +327,7 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
     HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, x0, ctx->X, ctx->U, ctx->status,
-                                  wind, s));
+                                  wind, ctx->order + 2 * B + 1, s));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(kite::launch_rk4_sens(ctx->mc, ctx->rc, B, ctx->X, ctx->U, ctx->AB, ctx->DEF, wind, s));
     if (ev) HIP_TRY(hipEventRecord(ev[2], s));
@@ -605,9 +606,10 @@ int kite_nmpc_create(const kite_params* params, const kite_nmpc_config* cfg, int
     }
     if (hipMalloc(&ctx->status, B * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->iters, 4 * B * sizeof(int32_t)) != hipSuccess ||
-        hipMalloc(&ctx->order, (2 * (size_t)B + 1) * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&ctx->order, (3 * (size_t)B + 2) * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&ctx->dconst, 4096) != hipSuccess) { free_ctx(ctx); delete ctx; return KITE_ENOMEM; }
     (void)hipMemset(ctx->status, 0, B * sizeof(int32_t));
+    (void)hipMemset(ctx->order, 0, (3 * (size_t)B + 2) * sizeof(int32_t));
     // [0, B): QP iterations of the last step; running sums since timing_start:
     // [B, 2B) QP iterations, [2B, 3B) steps ending outside the state box (status
     // bit 8), [3B, 4B) (node, state) pairs outside it (kite_nmpc_state_bound_stats)

@@ -84,39 +84,54 @@ __device__ void rk4_primal(const ModelConst& P, const double* x0, const double* 
 // simulation), x_0 pinned, theta/thetadot re-simulated exactly.  The per-kite
 // scalar logic runs on lane 0; the warm-start shift (the bulk of the bytes)
 // is a coalesced copy by the whole wave.
+//
+// FULL = false is the warm step without delay compensation, the common case:
+// no forward simulation is compiled in, so the kernel holds few registers and
+// runs at full occupancy (the full variant's inlined RK4 and closest-point
+// search take ~300 VGPRs, one wave per SIMD).  A kite it finds flagged for a
+// cold restart (status bit 1) goes on the cold list (cold[0] = count, entries
+// from cold[1]) instead, and k_prologue_cold runs the full variant for those.
+// Both variants execute the same arithmetic for a kite they both handle.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
-                                                 const double* __restrict__ x0in,
-                                                 double* __restrict__ X, double* __restrict__ U,
-                                                 int32_t* __restrict__ status, const double* __restrict__ wind) {
-    __shared__ double sx0[NX];
-    __shared__ double sUv[KITE_NMAX];
-    __shared__ int sWarm;
-    const int b = blockIdx.x;
+template <bool FULL>
+__device__ __forceinline__ void prologue_kite(const ModelConst& P, const RtiConst& C, int b, int warm,
+                                              const double* __restrict__ x0in, double* __restrict__ X,
+                                              double* __restrict__ U, int32_t* __restrict__ status,
+                                              const double* __restrict__ wind, int32_t* __restrict__ cold,
+                                              double* sx0, double* sUv, int* sWarm_) {
+    int& sWarm = *sWarm_;
     const int l = threadIdx.x;
-    if (b >= B) return;
     const int N = C.N;
     double* Xb = X + (size_t)b * (N + 1) * NX;
     double* Ub = U + (size_t)b * N * NU;
     int32_t st = 0;
+    if constexpr (!FULL) {
+        // launched on warm steps only: a kite flagged for a cold restart leaves
+        // for the cold list (block-uniform, the whole wave returns)
+        if (l == 0) sWarm = (status[b] & 1) ? -1 : 1;
+        __syncthreads();
+        if (sWarm < 0) {
+            if (l == 0) cold[1 + atomicAdd(cold, 1)] = b;
+            return;
+        }
+        __syncthreads();
+    }
     if (l == 0) {
         double x0[NX];
         for (int i = 0; i < NX; ++i) x0[i] = x0in[(size_t)b * NX + i];
         int wm = warm;
-        if (wm) {
+        if (FULL && wm && (status[b] & 1)) {
             // a non-finite plan (a NaN iterate of a previous step) cannot seed a
             // warm start: restart this kite cold, theta re-initialised by the
             // closest point and thetadot = 0 (the node's init, nmpf_node.cpp:225-236).
             // The previous epilogue flagged it (KITE_ST_NAN: non-finite X or U);
             // kite_nmpc_set_solution flags injected plans the same way.
-            if (status[b] & 1) {
-                wm = 0;
-                st |= 64;
-                x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
-                x0[14] = 0.0;
-            }
+            wm = 0;
+            st |= 64;
+            x0[13] = closest_point_dev(C, x0[6], x0[7], x0[8], isfinite(x0[13]) ? x0[13] : 0.0);
+            x0[14] = 0.0;
         }
-        if (wm && C.delay > 0.0) {
+        if (FULL && wm && C.delay > 0.0) {
             // transport-delay compensation (nmpf_node.cpp:206-221): predict the
             // measured kite state over `delay` under the previous u(t0); theta,
             // thetadot from the previous trajectory at t0 + delay
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
         if (x0[13] > twopi) { x0[13] -= twopi; st |= 16; }
         else if (x0[13] < -twopi) { x0[13] += twopi; st |= 16; }
         if (x0[0] < C.min_speed) { x0[0] = C.min_speed; st |= 4; }
-        if (!wm) {
+        if (FULL && !wm) {
             for (int k = 0; k < N; ++k)
                 for (int j = 0; j < NU; ++j) Ub[k * NU + j] = 0.5 * (C.lbu[j] + C.ubu[j]);
             for (int i = 0; i < NX; ++i) Xb[i] = x0[i];
@@ -195,6 +210,44 @@ __global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B
             th = thn; thd = thdn;
         }
         status[b] = st;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_prologue(ModelConst P, RtiConst C, int B, int warm,
+                                                 const double* __restrict__ x0in,
+                                                 double* __restrict__ X, double* __restrict__ U,
+                                                 int32_t* __restrict__ status, const double* __restrict__ wind) {
+    __shared__ double sx0[NX];
+    __shared__ double sUv[KITE_NMAX];
+    __shared__ int sWarm;
+    if ((int)blockIdx.x >= B) return;
+    prologue_kite<true>(P, C, blockIdx.x, warm, x0in, X, U, status, wind, nullptr, sx0, sUv, &sWarm);
+}
+// warm step, no delay compensation (run_step's common case)
+__global__ __launch_bounds__(64) void k_prologue_warm(ModelConst P, RtiConst C, int B,
+                                                      const double* __restrict__ x0in,
+                                                      double* __restrict__ X, double* __restrict__ U,
+                                                      int32_t* __restrict__ status, int32_t* __restrict__ cold) {
+    __shared__ double sx0[NX];
+    __shared__ double sUv[KITE_NMAX];
+    __shared__ int sWarm;
+    if ((int)blockIdx.x >= B) return;
+    prologue_kite<false>(P, C, blockIdx.x, 1, x0in, X, U, status, nullptr, cold, sx0, sUv, &sWarm);
+}
+// the kites k_prologue_warm put on the cold list, one per block in a
+// grid-stride loop (normally none: every block reads cold[0] = 0 and leaves)
+__global__ __launch_bounds__(64) void k_prologue_cold(ModelConst P, RtiConst C, const double* __restrict__ x0in,
+                                                      double* __restrict__ X, double* __restrict__ U,
+                                                      int32_t* __restrict__ status,
+                                                      const double* __restrict__ wind,
+                                                      const int32_t* __restrict__ cold) {
+    __shared__ double sx0[NX];
+    __shared__ double sUv[KITE_NMAX];
+    __shared__ int sWarm;
+    const int n = cold[0];
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        prologue_kite<true>(P, C, cold[1 + i], 1, x0in, X, U, status, wind, nullptr, sx0, sUv, &sWarm);
+        __syncthreads();
     }
 }
 
@@ -1952,8 +2005,16 @@ __global__ __launch_bounds__(64, 2) void k_closest_point(RtiConst C, int count, 
 // launch wrappers
 // ---------------------------------------------------------------------------
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
-                           double* X, double* U, int32_t* status, const double* wind, hipStream_t s) {
-    hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status, wind);
+                           double* X, double* U, int32_t* status, const double* wind, int32_t* cold,
+                           hipStream_t s) {
+    constexpr int PRO_COLD_GRID = 256;
+    if (warm && !(C.delay > 0.0)) {
+        hipLaunchKernelGGL(k_prologue_warm, dim3(B), dim3(64), 0, s, P, C, B, x0, X, U, status, cold);
+        hipLaunchKernelGGL(k_prologue_cold, dim3(B < PRO_COLD_GRID ? B : PRO_COLD_GRID), dim3(64), 0, s, P, C,
+                           x0, X, U, status, wind, cold);
+    } else {
+        hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status, wind);
+    }
     return hipGetLastError();
 }
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
@@ -2034,7 +2095,7 @@ __global__ __launch_bounds__(1024) void k_qp_order(int B, int K, const int32_t* 
                                                    int32_t* __restrict__ order, int32_t* __restrict__ lazy) {
     __shared__ int cnt[257];
     const int t = threadIdx.x;
-    if (t == 0) lazy[0] = 0;
+    if (t == 0) { lazy[0] = 0; lazy[B + 1] = 0; }     // and the prologue's cold list after it
     const int nb = (K < 255 ? K : 255) + 1;
     for (int i = t; i <= nb; i += 1024) cnt[i] = 0;
     __syncthreads();

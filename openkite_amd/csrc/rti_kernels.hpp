@@ -74,8 +74,11 @@ hipError_t launch_qp_ric(const RtiConst& C, const RicConst& R, const RtiConst* C
 
 // wind: per-kite constant world-frame wind (B x 3, m/s) or nullptr (the
 // reference model, no wind; kite_model.hpp kite_rhs<T, WIND>)
+// cold: B + 1 ints, the prologue's cold-restart list (count first; zero on
+// entry -- k_qp_order empties it every step)
 hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int warm, const double* x0,
-                           double* X, double* U, int32_t* status, const double* wind, hipStream_t s);
+                           double* X, double* U, int32_t* status, const double* wind, int32_t* cold,
+                           hipStream_t s);
 hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const double* X, const double* U,
                            double* AB, double* DEF, const double* wind, hipStream_t s);
 hipError_t launch_condense(const RtiConst& C, int B, const double* X, const double* U, const double* AB,
@@ -96,6 +99,7 @@ hipError_t launch_qp(const ModelConst& P, const RtiConst& C, int B, const double
                      hipStream_t s, hipEvent_t after_main = nullptr);
 // QP grid dispatch order: kites by the previous step's iteration count, most
 // first; also empties the lazy state-bound list (lazy[0] = 0, B + 1 entries)
+// and the prologue's cold list that follows it (lazy[B + 1] = 0)
 hipError_t launch_publish(int B, int N, const double* u0, const double* X, const double* U, const double* diag,
                           const int32_t* status, double* d_u0, double* d_traj, double* d_ctrl, double* d_diag,
                           int32_t* d_status, hipStream_t s);
