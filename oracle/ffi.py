@@ -123,6 +123,8 @@ def lib():
             "orc_set_wind_batch": (None, [dp, i]),
             "orc_set_ms_z0": (None, [d]),
             "orc_set_ipm_z0": (None, [d]),
+            "orc_set_ipm_gondzio": (None, [i]),
+            "orc_gondzio_solves": (ctypes.c_longlong, []),
             "orc_get_ipm_z0": (d, []),
             "orc_get_ms_z0": (d, []),
             "orc_msqp_build": (i, [dp, dp, i, i, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp, dp]),
@@ -301,6 +303,18 @@ def set_ms_z0(z0: float) -> float:
     old = L.orc_get_ms_z0()
     L.orc_set_ms_z0(float(z0))
     return old
+
+
+def set_ipm_gondzio(k: int) -> None:
+    """Study switch: up to k Gondzio centrality correctors in the oracle's
+    condensed IPM (tools only; 0 = the product rule, which the GPU kernels
+    implement)."""
+    lib().orc_set_ipm_gondzio(int(k))
+
+
+def gondzio_solves() -> int:
+    """Corrector solves since the last set_ipm_gondzio (tools only)."""
+    return int(lib().orc_gondzio_solves())
 
 
 def set_ipm_z0(z0: float) -> float:
