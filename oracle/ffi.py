@@ -124,6 +124,7 @@ def lib():
             "orc_set_ms_z0": (None, [d]),
             "orc_set_ipm_z0": (None, [d]),
             "orc_set_ipm_gondzio": (None, [i]),
+            "orc_set_ipm_study": (None, [d, d]),
             "orc_gondzio_solves": (ctypes.c_longlong, []),
             "orc_get_ipm_z0": (d, []),
             "orc_get_ms_z0": (d, []),
@@ -310,6 +311,12 @@ def set_ipm_gondzio(k: int) -> None:
     condensed IPM (tools only; 0 = the product rule, which the GPU kernels
     implement)."""
     lib().orc_set_ipm_gondzio(int(k))
+
+
+def set_ipm_study(tau: float = 0.995, s0: float = 0.1) -> None:
+    """Study switches: the condensed IPM's step-to-boundary floor and start
+    slack (tools only; the defaults are the product constants)."""
+    lib().orc_set_ipm_study(float(tau), float(s0))
 
 
 def gondzio_solves() -> int:
