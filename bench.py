@@ -286,7 +286,13 @@ def pmc_traffic(names, cfg_tag):
     tools/pmc_summary.py) whose recorded bench configuration is this run's;
     None if no profile matches."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")))
+    import re
+
+    def session_key(f):
+        # profiles/r05q_..., r05aa_...: round, then session letters (a..z, aa..)
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_hbm.json")), key=session_key)
     for f in reversed(files):
         d = json.load(open(f))
         if d.get("bench_config") != cfg_tag:
