@@ -287,6 +287,36 @@ def test_restart_on_nonfinite_plan_vs_oracle(kp, cfgv):
         g.close()
 
 
+def test_restart_on_nonfinite_plan_vs_oracle_n40(kp):
+    """The same at N = 40 (multiple-shooting QP): on a warm step the prologue
+    puts the two kites with a non-finite warm start on its cold-restart list
+    (k_prologue_warm -> k_prologue_cold), and they restart exactly as in the
+    oracle; the others continue warm."""
+    Nh, B = 40, 16
+    cv = ffi.cfg_vector(ffi.node_config(N=Nh))
+    x = x0_batch(B, offset=5100)
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(N=Nh), B)
+    Xo = np.zeros((B, Nh + 1, 15)); Uo = np.zeros((B, Nh, 4))
+    try:
+        for step in range(3):
+            if step == 2:
+                Xo[3, 5, 1] = np.nan
+                Uo[9, 0, 0] = np.inf
+                x[3, 13] = np.nan
+                g.set_solution(Xo, Uo)
+            r = g.step(x)
+            u0, diag, st = ffi.rti_step(kp, cv, Nh, M, K, x, Xo, Uo, warm=int(step > 0))
+            # bits 2 / 32 (converged, step safeguard) may differ only where the
+            # capped residuals straddle their thresholds (config-5 test); none here
+            np.testing.assert_array_equal(r["status"], st)
+            assert_ms_rti(rel_per_kite(r["traj"], Xo), r["diag"][:, 5], diag[:, 5], step)
+            x = Xo[:, 1, :].copy()
+        assert st[3] & 64 and st[9] & 64 and not np.any(np.delete(st, [3, 9]) & 64)
+        assert np.all(np.isfinite(r["traj"]))
+    finally:
+        g.close()
+
+
 def test_long_closed_loop_vs_oracle(kp, cfgv):
     """256 kites x 25 closed-loop steps along the oracle's trajectory: the
     synthetic kites slow down onto the vx >= 2 bound, where a few QPs become
