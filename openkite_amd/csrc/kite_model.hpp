@@ -70,13 +70,15 @@ __device__ __forceinline__ double fast_rcp(double d) {
     const double e = fma(-d, r, 1.0);
     return fma(r, fma(e, e, e), r);
 }
+// (the tangent formulas are written exactly as Dual2's, fma included, so that
+// the one-tangent sensitivity kernel k_rk4_sens1 reproduces k_rk4_sens2 bit for bit)
 __device__ __forceinline__ Dual operator/(Dual a, Dual b) {
     double ib = fast_rcp(b.v);
     double q = a.v * ib;
-    return mk(q, (a.t - q * b.t) * ib);
+    return mk(q, fma(-q, b.t, a.t) * ib);
 }
 __device__ __forceinline__ Dual operator/(Dual a, double b) { double ib = fast_rcp(b); return mk(a.v * ib, a.t * ib); }
-__device__ __forceinline__ Dual rcp(Dual a) { double r = fast_rcp(a.v); return mk(r, -a.t * r * r); }
+__device__ __forceinline__ Dual rcp(Dual a) { const double r = fast_rcp(a.v), nr2 = -r * r; return mk(r, a.t * nr2); }
 __device__ __forceinline__ double rcp(double a) { return 1.0 / a; }
 
 __device__ __forceinline__ double val(double a) { return a; }
@@ -93,7 +95,8 @@ __device__ __forceinline__ Dual dasin(Dual x, Dual cosv) { return mk(asin(x.v), 
 // atan2(y,x) when x^2+y^2 is already known
 __device__ __forceinline__ double datan2(double y, double x, double /*r2*/) { return atan2(y, x); }
 __device__ __forceinline__ Dual datan2(Dual y, Dual x, Dual r2) {
-    return mk(atan2(y.v, x.v), (x.v * y.t - y.v * x.t) * fast_rcp(r2.v));
+    const double ir = fast_rcp(r2.v);
+    return mk(atan2(y.v, x.v), fma(x.v, y.t, -(y.v * x.t)) * ir);
 }
 
 // ---------------------------------------------------------------------------
@@ -124,7 +127,7 @@ __device__ __forceinline__ Dual2 operator*(double c, Dual2 x) { return mk2(x.v *
 __device__ __forceinline__ Dual2 operator/(Dual2 x, Dual2 y) {
     const double iy = fast_rcp(y.v);
     const double q = x.v * iy;
-    return mk2(q, (x.a - q * y.a) * iy, (x.b - q * y.b) * iy);
+    return mk2(q, fma(-q, y.a, x.a) * iy, fma(-q, y.b, x.b) * iy);
 }
 __device__ __forceinline__ Dual2 operator/(Dual2 x, double c) {
     const double ic = fast_rcp(c);
@@ -146,7 +149,7 @@ __device__ __forceinline__ Dual2 dasin(Dual2 x, Dual2 cosv) {
 }
 __device__ __forceinline__ Dual2 datan2(Dual2 y, Dual2 x, Dual2 r2) {
     const double ir = fast_rcp(r2.v);
-    return mk2(atan2(y.v, x.v), (x.v * y.a - y.v * x.a) * ir, (x.v * y.b - y.v * x.b) * ir);
+    return mk2(atan2(y.v, x.v), fma(x.v, y.a, -(y.v * x.a)) * ir, fma(x.v, y.b, -(y.v * x.b)) * ir);
 }
 
 // two fp32 tangents (mixed precision, config sens_fp32 = 1, k_rk4_sens2<DualF2>),

@@ -322,6 +322,58 @@ __global__ __launch_bounds__(RK2_T, 1) void k_rk4_sens2(ModelConst P, int B, int
     }
 }
 
+// Latency form for small batches (B <= RK1_MAXB, fp64): ONE tangent per lane,
+// 16 lanes per (instance, interval), four instances per 64-thread block.
+// Each lane runs about 60 % of a Dual2 lane's instructions, so a batch too
+// small to fill the GPU (one kite: 20 intervals) finishes its RK4 chains
+// sooner; at large batches the Dual2 form's shared primal wins.
+// Same per-direction arithmetic as Dual2 (the operators are written alike).
+constexpr int RK1_T = 64, RK1_MAXB = 128;
+__global__ __launch_bounds__(RK1_T, 1) void k_rk4_sens1(ModelConst P, int B, int N, int M, double h,
+                                                        const double* __restrict__ X,
+                                                        const double* __restrict__ U,
+                                                        double* __restrict__ AB, double* __restrict__ DEF) {
+    const int d = threadIdx.x & 15;
+    const int b = blockIdx.x * (RK1_T / 16) + (threadIdx.x >> 4);
+    const int k = blockIdx.y;
+    if (b >= B) return;
+    const double* xk = X + ((size_t)b * (N + 1) + k) * NX;
+    const double* uk = U + ((size_t)b * N + k) * NU;
+    Dual x[NK], u[NKU];
+#pragma unroll
+    for (int i = 0; i < NK; ++i) x[i] = Dual(xk[i], d == i ? 1.0 : 0.0);
+#pragma unroll
+    for (int j = 0; j < NKU; ++j) u[j] = Dual(uk[j], d == NK + j ? 1.0 : 0.0);
+#pragma unroll 1
+    for (int m = 0; m < M; ++m) {
+        Dual xs[NK], acc[NK], kv[NK];
+#pragma unroll
+        for (int i = 0; i < NK; ++i) { xs[i] = x[i]; acc[i] = x[i]; }
+#pragma unroll 1
+        for (int st = 0; st < 4; ++st) {
+            kite_rhs<Dual, false>(P, xs, u, kv, nullptr);
+            const double wa = (st == 0 || st == 3) ? h / 6.0 : h / 3.0;
+            const double wn = (st < 2) ? 0.5 * h : h;
+#pragma unroll
+            for (int i = 0; i < NK; ++i) {
+                acc[i] = Dual(fma(wa, kv[i].v, acc[i].v), fma(wa, kv[i].t, acc[i].t));
+                xs[i] = Dual(fma(wn, kv[i].v, x[i].v), fma(wn, kv[i].t, x[i].t));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NK; ++i) x[i] = acc[i];
+    }
+    double* ab = AB + ((size_t)b * N + k) * (NK * 16);
+#pragma unroll
+    for (int i = 0; i < NK; ++i) ab[i * 16 + d] = x[i].t;
+    if (d == 0) {
+        const double* xn = X + ((size_t)b * (N + 1) + k + 1) * NX;
+        double* df = DEF + ((size_t)b * N + k) * NK;
+#pragma unroll
+        for (int i = 0; i < NK; ++i) df[i] = x[i].v - xn[i];
+    }
+}
+
 // fp64 multiple-shooting defects x+(x_k, u_k) - x_{k+1}, lane per (instance,
 // interval): the right-hand side of the QP when the sensitivities run in fp32
 __global__ __launch_bounds__(64, 2) void k_defects(ModelConst P, int B, int N, int M, double h,
@@ -2029,6 +2081,9 @@ hipError_t launch_rk4_sens(const ModelConst& P, const RtiConst& C, int B, const 
                                AB, DEF, nullptr);
         hipLaunchKernelGGL(k_defects, dim3((B * C.N + 63) / 64), dim3(64), 0, s, P, B, C.N, C.M, C.h, X, U, DEF,
                            wind);
+    } else if (!wind && B <= RK1_MAXB) {
+        hipLaunchKernelGGL(k_rk4_sens1, dim3((B + RK1_T / 16 - 1) / (RK1_T / 16), C.N), dim3(RK1_T), 0, s, P, B,
+                           C.N, C.M, C.h, X, U, AB, DEF);
     } else {
         if (wind)
             hipLaunchKernelGGL((k_rk4_sens2<Dual2, double, true>), grid2, dim3(RK2_T), 0, s, P, B, C.N, C.M, C.h, X,
