@@ -260,9 +260,15 @@ __host__ __device__ __forceinline__ void kite_rhs(const ModelConst& P, const T* 
     const T thr = u[0], dE = u[1], dR = u[2];
     V3<T> va = v;
     if constexpr (WIND) {
+        // the wind is a constant: its rotation multiplies by plain doubles
+        // (a dual-typed constant would carry zero tangents through every product)
         const T wwuu = qw * qw - dot3(qu, qu);
-        const V3<T> Wb = rot_body(qw, qu, wwuu, V3<T>{T(wnd[0]), T(wnd[1]), T(wnd[2])});
-        va = V3<T>{v.x - Wb.x, v.y - Wb.y, v.z - Wb.z};
+        const double W0 = wnd[0], W1 = wnd[1], W2 = wnd[2];
+        const T uv2 = 2.0 * (qu.x * W0 + qu.y * W1 + qu.z * W2);
+        const T cx = qu.y * W2 - qu.z * W1, cy = qu.z * W0 - qu.x * W2, cz = qu.x * W1 - qu.y * W0;
+        const T w2 = 2.0 * qw;
+        va = V3<T>{v.x - (wwuu * W0 + uv2 * qu.x - w2 * cx), v.y - (wwuu * W1 + uv2 * qu.y - w2 * cy),
+                   v.z - (wwuu * W2 + uv2 * qu.z - w2 * cz)};
     }
 
     // airspeed, angles (kite.cpp:197-202)
@@ -298,9 +304,13 @@ __host__ __device__ __forceinline__ void kite_rhs(const ModelConst& P, const T* 
     const T uu = dot3(qu, qu);
     const T ww_uu = qw * qw - uu;
 
-    // gravity q^-1 [0,0,0,g] q (kite.cpp:237-240)
-    const V3<T> gz{T(0.0), T(0.0), T(kGravity)};
-    const V3<T> Gb = rot_body(qw, qu, ww_uu, gz);
+    // gravity q^-1 [0,0,0,g] q (kite.cpp:237-240): rot_body with v = (0, 0, g)
+    // written with its nonzero terms only (x * 0 is not folded for doubles: a
+    // dual-typed (0, 0, g) would spend a third of the rotation on zeros)
+    const T guv2 = 2.0 * (qu.z * kGravity);
+    const T gcx = qu.y * kGravity, gcy = -(qu.x * kGravity);
+    const T gw2 = 2.0 * qw;
+    const V3<T> Gb{guv2 * qu.x - gw2 * gcx, guv2 * qu.y - gw2 * gcy, ww_uu * kGravity + guv2 * qu.z};
 
     // tether (kite.cpp:247-265)
     const T d2 = dot3(r, r);

@@ -45,8 +45,8 @@ Per instance:
 """
 from __future__ import annotations
 
-F_F = 320      # primal RHS (tools/flopcount.cpp)
-F_T = 566      # one tangent direction through the RHS
+F_F = 303      # primal RHS (tools/flopcount.cpp)
+F_T = 547      # one tangent direction through the RHS
 NK = 13
 NDIR = 16
 

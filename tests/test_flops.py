@@ -26,8 +26,8 @@ def test_rhs_op_counts_rederived(tmp_path):
 
 def test_per_instance_figures():
     # N = 20, M = 2
-    assert flops.rk4_sens_per_interval(2) == 82080
-    assert abs(flops.rk4_sens(20, 2) / 1e6 - 1.64) < 0.01
+    assert flops.rk4_sens_per_interval(2) == 79512
+    assert abs(flops.rk4_sens(20, 2) / 1e6 - 1.59) < 0.01
     assert abs(flops.condense_dense(20) / 1e6 - 0.78) < 0.01
     assert abs(flops.condense(20) / 1e6 - 0.401) < 0.001
     assert abs(flops.qp_per_iteration_dense(20) / 1e6 - 0.383) < 0.001
