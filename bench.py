@@ -551,6 +551,10 @@ def main():
                        "meas_noise": args.meas_noise, "rate_bound": args.rate_bound,
                        "qp_kernel": ok.resolve_qp_kernel(args.qp_kernel, N), "qp_lm": cfg.qp_lm,
                        "qp_soft_weight": cfg.qp_soft_weight,
+                       # the measurement window: the synthetic loop is a transient
+                       # (DESIGN 6), so numbers compare only at equal windows
+                       "timed_steps": args.steps, "warmup_steps": args.warmup,
+                       "timing_stride": TIMING_STRIDE,
                        "backend": dist.get_backend() if distributed else "none"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -41,7 +41,6 @@ extern "C" {
                                       (arbitrary closed paths); delay_steps default 16;
                                    4: kite_nmpc_state_bound_stats (no config change);
                                    5: kite_nmpc_set_wind (no config change);
-                                      qp_soft_weight must exceed 40 (was 20);
                                    6: kernel_times / timing_read report a sixth
                                       entry, the main QP kernel alone;
                                    7: kite_nmpc_timing_start_sampled (events on
@@ -142,7 +141,7 @@ typedef struct kite_nmpc_config {
                               scaled units (1e3); the QP stays feasible when the linearised
                               dynamics cannot meet the box over the horizon.  Must exceed
                               40 = 2 z0 (the IPM's start multiplier, so every soft row starts
-                              dual feasible): smaller values give KITE_EINVAL (since API 5)    */
+                              dual feasible): smaller values give KITE_EINVAL                 */
     double qp_lm;          /* qp_kernel 3: Levenberg-Marquardt term lm/2 ||step||^2 on every QP
                               variable, scaled units (10); leaves the RTI fixed point unchanged.
                               qp_lm = 0 with qp_soft_weight = 1e6 at N = 20: the condensed

@@ -77,6 +77,10 @@ struct kite_nmpc_ctx {
     size_t scratch_bytes = 0;
     hipEvent_t ev[KITE_NEV] = {};
     bool timed_step = false;
+    // the prologue's cold-restart count (order + 2B + 1) is zeroed by k_qp_order
+    // later in the same step; set while a step is between the two launches, so
+    // a step that returned early in between zeroes it before the next prologue
+    bool cold_dirty = false;
     // event ring for timing a whole run without host syncs (kite_nmpc_timing_start),
     // KITE_NEV events per step
     std::vector<hipEvent_t> ring;
@@ -326,6 +330,8 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
         ev = ctx->ev;
     if (ev) HIP_TRY(hipEventRecord(ev[0], s));
     const double* wind = ctx->has_wind ? ctx->wind : nullptr;
+    if (ctx->cold_dirty) HIP_TRY(hipMemsetAsync(ctx->order + 2 * B + 1, 0, sizeof(int32_t), s));
+    ctx->cold_dirty = true;
     HIP_TRY(kite::launch_prologue(ctx->mc, ctx->rc, B, ctx->warm ? 1 : 0, x0, ctx->X, ctx->U, ctx->status,
                                   wind, ctx->order + 2 * B + 1, s));
     if (ev) HIP_TRY(hipEventRecord(ev[1], s));
@@ -337,6 +343,7 @@ int run_step(kite_nmpc_ctx* ctx, const double* x0) {
                                       ctx->Hbb, s));
     // QP dispatch order from the previous step's iteration counts (ctx->iters[0, B))
     HIP_TRY(kite::launch_qp_order(ctx->rc, B, ctx->iters, ctx->order, ctx->order + B, s));
+    ctx->cold_dirty = false;
     if (ev) HIP_TRY(hipEventRecord(ev[3], s));
     if (ctx->ric) {
         constexpr size_t roff = (sizeof(kite::RtiConst) + 255) / 256 * 256;

@@ -98,7 +98,7 @@ __device__ __forceinline__ void prologue_kite(const ModelConst& P, const RtiCons
                                               const double* __restrict__ x0in, double* __restrict__ X,
                                               double* __restrict__ U, int32_t* __restrict__ status,
                                               const double* __restrict__ wind, int32_t* __restrict__ cold,
-                                              double* sx0, double* sUv, int* sWarm_) {
+                                              double* sx0, double* sUv, int* sWarm_, int B = 0) {
     int& sWarm = *sWarm_;
     const int l = threadIdx.x;
     const int N = C.N;
@@ -111,7 +111,10 @@ __device__ __forceinline__ void prologue_kite(const ModelConst& P, const RtiCons
         if (l == 0) sWarm = (status[b] & 1) ? -1 : 1;
         __syncthreads();
         if (sWarm < 0) {
-            if (l == 0) cold[1 + atomicAdd(cold, 1)] = b;
+            if (l == 0) {
+                const int slot = atomicAdd(cold, 1);   // < B: launch_prologue zeroes the count first
+                if (slot < B) cold[1 + slot] = b;
+            }
             return;
         }
         __syncthreads();
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(64) void k_prologue_warm(ModelConst P, RtiConst C, 
     __shared__ double sUv[KITE_NMAX];
     __shared__ int sWarm;
     if ((int)blockIdx.x >= B) return;
-    prologue_kite<false>(P, C, blockIdx.x, 1, x0in, X, U, status, nullptr, cold, sx0, sUv, &sWarm);
+    prologue_kite<false>(P, C, blockIdx.x, 1, x0in, X, U, status, nullptr, cold, sx0, sUv, &sWarm, B);
 }
 // the kites k_prologue_warm put on the cold list, one per block in a
 // grid-stride loop (normally none: every block reads cold[0] = 0 and leaves)
@@ -240,11 +243,11 @@ __global__ __launch_bounds__(64) void k_prologue_cold(ModelConst P, RtiConst C, 
                                                       double* __restrict__ X, double* __restrict__ U,
                                                       int32_t* __restrict__ status,
                                                       const double* __restrict__ wind,
-                                                      const int32_t* __restrict__ cold) {
+                                                      const int32_t* __restrict__ cold, int B) {
     __shared__ double sx0[NX];
     __shared__ double sUv[KITE_NMAX];
     __shared__ int sWarm;
-    const int n = cold[0];
+    const int n = min(cold[0], B);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         prologue_kite<true>(P, C, cold[1 + i], 1, x0in, X, U, status, wind, nullptr, sx0, sUv, &sWarm);
         __syncthreads();
@@ -877,13 +880,18 @@ __global__ __launch_bounds__(64 * CondenseGeom<NR>::NW) __attribute__((amdgpu_wa
 // instruction itself (it keeps a v_mov_b64_dpp + v_fmac_f64 pair), and its
 // hazard recognizer does not look into inline asm: the leading s_nop 1 covers
 // the two wait states a VALU write of the DPP source needs (the column comes
-// from a global load, but the register allocator may copy it).
+// from a global load, but the register allocator may copy it), and the
+// trailing s_nop 1 the two a DPP / permlane after the block needs if it reads
+// an nv register the last fmac wrote.  Every lane of a row needs the
+// broadcast, so the block is correct only with the full EXEC mask:
+// k_condense20 calls it only under the wave-uniform `!last` (64-lane blocks,
+// no divergent branch around it).
 #define KITE_FMAC_DPP(I) "v_fmac_f64_dpp %" #I ", %13, %14 row_newbcast:" #I " row_mask:0xf bank_mask:0xf\n\t"
 __device__ __forceinline__ void fmac_col13(double (&nv)[NK], double a, double vj) {
     asm("s_nop 1\n\t"
         KITE_FMAC_DPP(0) KITE_FMAC_DPP(1) KITE_FMAC_DPP(2) KITE_FMAC_DPP(3) KITE_FMAC_DPP(4)
         KITE_FMAC_DPP(5) KITE_FMAC_DPP(6) KITE_FMAC_DPP(7) KITE_FMAC_DPP(8) KITE_FMAC_DPP(9)
-        KITE_FMAC_DPP(10) KITE_FMAC_DPP(11) KITE_FMAC_DPP(12)
+        KITE_FMAC_DPP(10) KITE_FMAC_DPP(11) KITE_FMAC_DPP(12) "s_nop 1"
         : "+v"(nv[0]), "+v"(nv[1]), "+v"(nv[2]), "+v"(nv[3]), "+v"(nv[4]), "+v"(nv[5]), "+v"(nv[6]),
           "+v"(nv[7]), "+v"(nv[8]), "+v"(nv[9]), "+v"(nv[10]), "+v"(nv[11]), "+v"(nv[12])
         : "v"(a), "v"(vj));
@@ -2063,7 +2071,7 @@ hipError_t launch_prologue(const ModelConst& P, const RtiConst& C, int B, int wa
     if (warm && !(C.delay > 0.0)) {
         hipLaunchKernelGGL(k_prologue_warm, dim3(B), dim3(64), 0, s, P, C, B, x0, X, U, status, cold);
         hipLaunchKernelGGL(k_prologue_cold, dim3(B < PRO_COLD_GRID ? B : PRO_COLD_GRID), dim3(64), 0, s, P, C,
-                           x0, X, U, status, wind, cold);
+                           x0, X, U, status, wind, cold, B);
     } else {
         hipLaunchKernelGGL(k_prologue, dim3(B), dim3(64), 0, s, P, C, B, warm, x0, X, U, status, wind);
     }

@@ -823,6 +823,32 @@ def test_rk4_sens_hot_kernel_ragged_batch(kp, fp32):
         assert rel(A[i], Ar) < stol and rel(Bm[i], Br) < stol, (i, rel(A[i], Ar), rel(Bm[i], Br))
 
 
+def test_rk4_sens1_equals_sens2_across_the_switch(kp):
+    """launch_rk4_sens takes the one-tangent kernel k_rk4_sens1 for B <= 128
+    (no wind) and k_rk4_sens2 above.  The same 128 items run once alone
+    (k_rk4_sens1) and once as the first 128 of 129 (k_rk4_sens2): x+, A and B
+    are bitwise equal (both kernels use the same tangent
+    formulas), and both match the oracle."""
+    count = 129
+    x = x0_batch(count, offset=911)
+    rng = np.random.default_rng(23)
+    x[:, :13] += rng.normal(scale=0.05, size=(count, 13))
+    x[:, 13:] = rng.normal(size=(count, 2))
+    u = np.column_stack([rng.uniform(0.1, 0.15, count), rng.uniform(-0.12, 0.12, (count, 2)),
+                         rng.uniform(-5, 5, count)])
+    g = ok.BatchNMPC(ok.load_properties(), ok.default_config(), 1)
+    try:
+        x1, A1, B1 = g.rk4_sens(x[:128], u[:128], 0.05, 2)      # k_rk4_sens1
+        x2, A2, B2 = g.rk4_sens(x, u, 0.05, 2)                  # k_rk4_sens2
+    finally:
+        g.close()
+    assert np.array_equal(x1, x2[:128])
+    assert np.array_equal(A1, A2[:128]) and np.array_equal(B1, B2[:128])
+    for i in (0, 63, 127):
+        xr, Ar, Br = ffi.rk4_sens(kp, x[i], u[i], 0.025, 2)
+        assert rel(x1[i], xr) < 1e-12 and rel(A1[i], Ar) < 1e-10 and rel(B1[i], Br) < 1e-10, i
+
+
 @pytest.mark.parametrize("Nh", [20, 40])
 def test_captured_host_step_matches_uncaptured(Nh):
     """kite_nmpc_step runs a captured HIP graph with pinned staging (batch-1
