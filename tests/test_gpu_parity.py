@@ -397,6 +397,52 @@ def test_full_batch_properties():
         g1.close(); g2.close()
 
 
+@pytest.mark.parametrize("Nh", [20, 40])
+def test_ric_two_wave_kernel_equals_single_wave(Nh):
+    """k_qp_ric<.., 2> (B <= SIMDs / 2: a second wave per kite runs the
+    predictor's backward vector sweep beside the factorisation) against the
+    single-wave kernel, forced by KITE_RIC_WAVES: the same closed loop at
+    B = 96, every output bitwise equal.  Then batch invariance across the
+    dispatch switch: the first 96 kites of a 4096-kite batch (single wave)
+    against the same 96 alone (two waves, the automatic choice)."""
+    import os
+    B = 96
+    x0 = x0_batch(B, offset=2400)
+    cfg = ok.default_config(N=Nh, qp_kernel=3)
+    res = {}
+    for w in ("1", "2"):
+        os.environ["KITE_RIC_WAVES"] = w
+        try:
+            g = ok.BatchNMPC(ok.load_properties(), cfg, B)
+            x, out = x0.copy(), []
+            for _ in range(4):
+                r = g.step(x)
+                out.append((r["u0"].copy(), r["traj"].copy(), r["ctrl"].copy(), r["status"].copy(),
+                            g.qp_stats()[0].copy(), g.qp_stats()[1].copy()))
+                x = r["traj"][:, 1, :].copy()
+            g.close()
+        finally:
+            del os.environ["KITE_RIC_WAVES"]
+        res[w] = out
+    for a, b in zip(res["1"], res["2"]):
+        for u, v in zip(a, b):
+            np.testing.assert_array_equal(u, v)
+    assert np.all(np.isfinite(res["2"][-1][1]))
+    if Nh == 40:
+        xb = x0_batch(4096)
+        xb[:B] = x0
+        g1 = ok.BatchNMPC(ok.load_properties(), cfg, 4096)
+        try:
+            x = xb
+            for s in range(4):
+                r = g1.step(x)
+                np.testing.assert_array_equal(r["traj"][:B], res["2"][s][1])
+                np.testing.assert_array_equal(r["u0"][:B], res["2"][s][0])
+                x = r["traj"][:, 1, :].copy()
+        finally:
+            g1.close()
+
+
 @pytest.mark.parametrize("qp_kernel", [1, 2, 3])
 def test_qp_iteration_sum_matches_per_step_counts(qp_kernel):
     """kite_nmpc_qp_iteration_sum (bench.py's FLOP count) = the per-step

@@ -6,7 +6,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-os.environ["KITE_NMPC_LIB"] = os.path.join(REPO, "openkite_amd", "lib", "libkite_nmpc_prof.so")
+os.environ.setdefault("KITE_NMPC_LIB", os.path.join(REPO, "openkite_amd", "lib", "libkite_nmpc_prof.so"))
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import openkite_amd as ok  # noqa: E402
