@@ -4,7 +4,7 @@
 # and the config-5 per-GPU latency probe for both variants in one session
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r06c; mkdir -p $OUT
+OUT=gpurun_out/${TAG:-r06c}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k two_wave --timeout 120 --timeout-method thread > $OUT/pytest_two_wave.log 2>&1 || { echo "two-wave test failed"; tail -30 $OUT/pytest_two_wave.log; exit 1; }
 tail -1 $OUT/pytest_two_wave.log
 KITE_RIC_WAVES=1 timeout -k 10 200 python tools/ric_latency_probe.py 512 20 5 > $OUT/latency512_w1.txt 2>&1 || { echo probe1 failed; exit 1; }
