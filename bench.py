@@ -480,7 +480,10 @@ def main():
         # sums restarted by timing_start), not just the last step
         mean_it = it_sum / float(B * args.steps)
         ric = ok.resolve_qp_kernel(args.qp_kernel, N) == 3
-        fl = flops.rti_ric(N, args.substeps, mean_it) if ric else flops.rti(N, args.substeps, mean_it)
+        # k_qp_tiled (qp_kernel 2 at N = 20) skips most residual products (recursive
+        # residuals): counted as a lower bound (flops.qp)
+        rec = not ric and N == 20 and ok.resolve_qp_kernel(args.qp_kernel, N) == 2
+        fl = flops.rti_ric(N, args.substeps, mean_it) if ric else flops.rti(N, args.substeps, mean_it, rec)
         kernels = ["prologue", "rk4_sens", "condense", "qp"]
         avg_ms = {k: ksum[k] / max(1, nrec) for k in kernels + ["qp_main"]}
         dom = max(kernels, key=lambda k: avg_ms[k])
@@ -492,7 +495,7 @@ def main():
         achieved = dom_flops / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else 0.0
         alt = {}
         if dom == "qp" and not ric:
-            qm = flops.qp_models(N, mean_it)
+            qm = flops.qp_models(N, mean_it, rec)
             alt = {f"frac_{k}_count": round(qm[k] * B / (dom_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS, 5)
                    for k in ("dense", "survey")}
         rti_flops = fl["total"] * B / (ksum["total"] / max(1, nrec) * 1e-3) / 1e12

@@ -1484,6 +1484,8 @@ constexpr double IPM_S0 = 0.1, IPM_Z0 = 20.0, IPM_FREEZE = 1e-10, IPM_TAU = 0.99
 // while a rounding floor of the stationarity residual keeps the test above the
 // freeze; continuing drives s, z to underflow and the Newton system to NaN
 constexpr double IPM_MU_FLOOR = 1e-20;
+// k_qp_tiled's recursive residuals (oracle cfg C_qp_rec, qp_tiled.inc)
+constexpr double QP_REC_THR = 1e-6;
 __device__ __forceinline__ int pk(int i, int c) { return (i * (i + 1)) / 2 + c; }
 
 // row of element e in a row-wise packed lower triangle

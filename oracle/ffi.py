@@ -73,6 +73,9 @@ def node_config(N: int = 20, dt: float = 0.05) -> Dict:
                                       # state rows (qp_form 0, qp_kernel 2), otherwise the
                                       # multiple-shooting QP (qp_form 1, qp_kernel 3)
         soft_weight=1e3, lm=10.0,     # kite_nmpc_default_config qp_soft_weight, qp_lm
+        qp_rec=1e-6 if N == 20 else 0.0,   # condensed IPM: recursive residuals above 1e-6 as k_qp_tiled
+                                           # (qp_kernel 2 at N = 20); 0 = exact each iteration (k_qp,
+                                           # k_qp_lds: qp_kernel 1, other horizons)
     )
 
 
@@ -84,8 +87,9 @@ def cfg_vector(c: Dict) -> np.ndarray:
     F = np.zeros((3, 17))
     if c.get("path_K", 0):
         F[:] = np.asarray(c["path_fourier"], dtype=np.float64).reshape(3, 17)
-    a = np.concatenate([np.array(v, dtype=np.float64), F.reshape(-1)])
-    assert a.size == 132
+    a = np.concatenate([np.array(v, dtype=np.float64), F.reshape(-1),
+                        np.array([c.get("qp_rec", 1e-6 if c.get("N", 20) == 20 else 0.0)], dtype=np.float64)])
+    assert a.size == 133
     return a
 
 

@@ -399,12 +399,12 @@ def test_full_batch_properties():
 
 @pytest.mark.parametrize("Nh", [20, 40])
 def test_ric_two_wave_kernel_equals_single_wave(Nh):
-    """k_qp_ric<.., 2> (B <= SIMDs / 2: a second wave per kite runs the
-    predictor's backward vector sweep beside the factorisation) against the
-    single-wave kernel, forced by KITE_RIC_WAVES: the same closed loop at
-    B = 96, every output bitwise equal.  Then batch invariance across the
-    dispatch switch: the first 96 kites of a 4096-kite batch (single wave)
-    against the same 96 alone (two waves, the automatic choice)."""
+    """k_qp_ric<.., 2> (B <= SIMDs / 2: a sweep wave and an elementwise
+    wave per kite) against the single-wave kernel, forced by
+    KITE_RIC_WAVES: the same closed loop at B = 96, every output bitwise
+    equal.  Then batch invariance across the dispatch switch: the first 96
+    kites of a 4096-kite batch (single wave) against the same 96 alone (two
+    waves, the automatic choice)."""
     import os
     B = 96
     x0 = x0_batch(B, offset=2400)
@@ -472,7 +472,9 @@ def test_qp_kernels_vs_oracle(kp, qp_kernel):
     """Both condensed-QP kernels (1 = wave-scalar, 2 = MFMA-tiled) against the
     oracle's condensed QP (qp_form 0)."""
     B = 16
-    cfgv = condensed_cfgv()
+    # k_qp (1) evaluates its residuals exactly every iteration, k_qp_tiled (2)
+    # recursively above 1e-6 (oracle cfg qp_rec)
+    cfgv = ffi.cfg_vector(dict(ffi.node_config(N=N), qp_form=0, qp_rec=0.0 if qp_kernel == 1 else 1e-6))
     x = x0_batch(B, offset=2000)
     cfg = ok.default_config()
     cfg.qp_kernel = qp_kernel
