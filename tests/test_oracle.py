@@ -232,6 +232,33 @@ def test_qp_sensitivity_envelope(kp, cfgv):
     print(f"condensed QP envelope: {e.size} frozen solves, median {np.median(e):.1e}, max {e.max():.1e}")
 
 
+def test_recursive_residuals_keep_the_iterations(kp):
+    """The condensed IPM's recursive residuals (cfg qp_rec, k_qp_tiled's rule,
+    DESIGN 4.3): along a closed loop, each step solved from the same inputs
+    with exact residuals and with recursive ones above 1e-6 takes the same
+    number of IPM iterations, and the committed steps agree within the QP's
+    perturbation envelope (COND_ENVELOPE), the typical kite at rounding level."""
+    from tests.test_gpu_parity import COND_ENVELOPE, x0_batch
+    N, M, K, B = 20, 2, 16, 48
+    base = dict(ffi.node_config(N=N), qp_form=0)
+    cv_exact, cv_rec = ffi.cfg_vector(dict(base, qp_rec=0.0)), ffi.cfg_vector(dict(base, qp_rec=1e-6))
+    assert ffi.cfg_vector(base)[132] == 1e-6                 # the N = 20 default is k_qp_tiled's rule
+    x = x0_batch(B, offset=4100)
+    X = np.zeros((B, N + 1, 15)); U = np.zeros((B, N, 4))
+    d = []
+    for step in range(5):
+        Xr, Ur = X.copy(), U.copy()
+        ie, ir = np.zeros(B, dtype=np.int32), np.zeros(B, dtype=np.int32)
+        ffi.rti_step(kp, cv_exact, N, M, K, x, X, U, warm=int(step > 0), nthreads=8, iters=ie)
+        ffi.rti_step(kp, cv_rec, N, M, K, x, Xr, Ur, warm=int(step > 0), nthreads=8, iters=ir)
+        np.testing.assert_array_equal(ie, ir)
+        d.append(np.maximum(np.abs(Xr - X).reshape(B, -1).max(1) / np.maximum(1, np.abs(X).reshape(B, -1).max(1)),
+                            np.abs(Ur - U).reshape(B, -1).max(1) / np.maximum(1, np.abs(U).reshape(B, -1).max(1))))
+        x = X[:, 1, :].copy()
+    d = np.concatenate(d)
+    assert d.max() < COND_ENVELOPE and np.median(d) < 1e-8, (d.max(), np.median(d))
+
+
 def test_delay_compensation_prologue(kp):
     """Delay compensation (nmpf_node.cpp:206-221) in the oracle prologue: kite
     state predicted over 0.1 s under the previous u(t0) with 16 RK4 substeps,
