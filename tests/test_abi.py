@@ -139,3 +139,32 @@ def test_create_fails_loudly_without_device_and_validates():
         with pytest.raises(ok.KiteNmpcError) as e:
             ok.BatchNMPC(p, ok.default_config(), 4)
         assert e.value.code == nmpc.KITE_ENODEV
+
+
+def test_two_wave_ric_hand_overs_are_ds_only():
+    """The two-wave k_qp_ric raises its LDS counters without an lgkmcnt wait
+    (qp_ric.inc, ric_publish): that relies on every LDS access of the kernel
+    being a DS instruction, executed in issue order.  A flat (generic-address)
+    load or store could reach LDS out of that order, so the built kernels must
+    contain none."""
+    import sys
+    sys.path.insert(0, os.path.join(ok.nmpc.REPO, "tools"))
+    from kernel_resources import code_objects
+    cos = [co for triple, co in code_objects(nmpc.LIB_PATH) if "gfx950" in triple]
+    assert cos
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not in this image")
+    import tempfile
+    kernels = []
+    for co in cos:                                   # one code object per translation unit
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            asm = subprocess.run([objdump, "-d", "--no-show-raw-insn", f.name], check=True, capture_output=True,
+                                 text=True).stdout
+        kernels += re.split(r"\n(?=[0-9a-f]+ <)", asm)
+    ric = [k for k in kernels if re.match(r"[0-9a-f]+ <_ZN4kite8k_qp_ric", k)]
+    assert len(ric) >= 2
+    for k in ric:
+        assert "flat_" not in k, k.splitlines()[0]
