@@ -17,8 +17,8 @@ from tests.test_gpu_parity import x0_batch  # noqa: E402
 
 EV = 18
 NAMES = {
-    8: "M residual pass done (1)",
-    0: "S past (1)",
+    8: "M Sigma + test published (1)",
+    0: "S has Sigma (1)",
     1: "S factor done",
     9: "M pred vector backward done",
     2: "S past (4)",
